@@ -1,0 +1,260 @@
+#!/usr/bin/env python3
+"""Benchmark: decoded frames/s at N=64800, 50 BP iterations (BASELINE.json metric).
+
+One process per GPU (torch.distributed over RCCL for N > 1).  Frames are
+independent, so every rank decodes its own batch (weak scaling; no collective
+on the data path); the only collective is the final all-reduce of the BER/FER
+counters plus the max-over-ranks of the timed region.
+
+A "step" = one pass of the hot path over one batch of B frames resident in HBM:
+  --workload dvbs2_4pam   (default, configs[2]): batched Decoder._decode of B
+                           frames, max_iterations=50, EsN0 3.0 dB (every frame runs
+                           all 50 iterations: the worst case / headline).
+  --workload dvbs2_16pam  (configs[3]): fused NoiseMapper soft demap (16-PAM) ->
+                           decode of B frames.
+Inputs (symbols, AWGN, Bob's x_hat/n_hat/word/syndrome, and for dvbs2_4pam the
+LAPPRs) are generated on the GPU before the timed region.
+
+The JSON line carries the roofline of the dominant kernel (the degree-7 check
+sweep k_check<7>, timed with hipEvents on its launch stream inside the timed
+region) and a CPU baseline (the oracle restatement, OpenMP over frames, on a
+bounded sample, rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "qam-reconciliation_amd"))
+
+METRIC = "decoded frames/sec @ N=64800, 50 BP iters; achieved HBM GB/s vs roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--workload", default="dvbs2_4pam", choices=["dvbs2_4pam", "dvbs2_16pam", "reg1008_4pam"])
+    p.add_argument("--batch", type=int, default=4096, help="frames per GPU")
+    p.add_argument("--snr", type=float, default=None, help="EsN0 [dB] (default per workload)")
+    p.add_argument("--max-iter", type=int, default=50)
+    p.add_argument("--alpha", type=float, default=1.0)
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
+    p.add_argument("--no-roofline", action="store_true", help="skip per-kernel event timing")
+    return p.parse_args()
+
+
+def setup_dist(args):
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def check_class_bytes(vid, cid, degree, B):
+    """Algorithmic bytes of one launch of the degree-`degree` check kernel over B
+    frames: c2v read + write (16 B per edge), the unique posteriors it gathers
+    (8 B per adjacent variable), the syndrome byte per check and the active flag
+    per frame (SURVEY.md 8(d) B_it, restricted to that launch)."""
+    deg = np.bincount(cid)
+    cls = np.flatnonzero(deg == degree)
+    mask = np.isin(cid, cls)
+    E_d = int(mask.sum())
+    V_d = int(np.unique(vid[mask]).size)
+    C_d = int(cls.size)
+    return (16 * E_d + 8 * V_d + C_d) * B + B, dict(E=E_d, V=V_d, C=C_d)
+
+
+def cpu_baseline(args, vid, cid, pipe, batch, lappr_host_fn, budget_s):
+    """Oracle restatement on the host cores for ~budget_s seconds of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = os.cpu_count() or 1
+    cores = max(1, min(aff, int(os.environ.get("OMP_NUM_THREADS", aff))))
+    code = O.OracleCode(vid, cid)
+    nfr = min(batch.B, cores)
+    synd = batch.synd[:, :nfr].cpu().numpy().T.copy()
+    if args.workload == "dvbs2_16pam":
+        nm = O.OracleNoiseMapper(4, 2.0, pipe.noise_var, np.array([0, 1] * 8, np.uint8))
+        nh = batch.nhat[:, :nfr].cpu().numpy().T.copy()
+        xs = batch.x[:, :nfr].cpu().numpy().T.copy()
+    else:
+        L = lappr_host_fn(nfr)
+    frames, t0 = 0, time.perf_counter()
+    rounds = 0
+    while True:
+        if args.workload == "dvbs2_16pam":
+            L = np.stack([nm.demap_lappr_array(nh[f], xs[f], nthreads=cores) * args.alpha for f in range(nfr)])
+        code.decode_batch(L, synd, args.max_iter, nthreads=cores)
+        frames += nfr
+        rounds += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or rounds >= 50:
+            break
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return {"value": frames / el, "unit": "frames/s", "cores": cores, "kind": "port",
+            "sample": f"{frames} frames ({rounds} rounds x {nfr}) of the same workload in {el:.1f} s, "
+                      f"oracle/qamr_oracle.c (gcc -O2 -ffp-contract=off, OpenMP over frames) on {cpu_model}"}
+
+
+def main():
+    args = parse()
+    import torch
+
+    world, rank, local = setup_dist(args)
+    import qamr
+    from qamr import codes
+    from qamr.pipeline import SofteningPipeline
+
+    if qamr.device_count() <= 0:
+        raise SystemExit("bench: no HIP device")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    if args.workload == "reg1008_4pam":
+        vid, cid = codes.regular_code(1008)
+        bps, snr = 2, (3.0 if args.snr is None else args.snr)
+        code_name = "reg-(3,6) N=1008"
+    else:
+        vid, cid = codes.dvbs2_like_half()
+        bps = 4 if args.workload == "dvbs2_16pam" else 2
+        snr = args.snr if args.snr is not None else (13.0 if bps == 4 else 3.0)
+        code_name = "DVB-S2-rate-1/2-profile IRA N=64800"
+    dec = qamr.Decoder(vid, cid, device=local)
+    pipe = SofteningPipeline(dec, bps=bps, snr_db=snr, batch=args.batch, alpha=args.alpha,
+                             max_iterations=args.max_iter, device=local)
+    gen = torch.Generator(device=dev).manual_seed(args.seed * 1000 + rank)
+    batch = pipe.generate(gen)
+    fused = args.workload == "dvbs2_16pam"
+    lappr = pipe.demap(batch)  # input LAPPRs (re-computed inside each step when fused)
+    final = torch.empty_like(lappr)
+    succ = torch.empty(batch.B, dtype=torch.uint8, device=dev)
+    its = torch.empty(batch.B, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        if fused:
+            pipe.demap(batch, out=lappr)
+        pipe.decode(lappr, batch, final, succ, its)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    if not args.no_roofline:
+        qamr.profile_reset()
+        qamr.profile_enable(True)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    qamr.profile_enable(False)
+
+    # BER/FER bookkeeping of the last step (and the only data-path-free collective)
+    pipe.count(final, batch, succ, its)
+    counters = pipe.counters.clone()
+    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        dist.all_reduce(counters, op=dist.ReduceOp.SUM)
+    elapsed = float(t_max.item())
+    total_frames = world * batch.B * args.steps
+    value = total_frames / elapsed
+
+    roof = None
+    kstats = {}
+    if not args.no_roofline:
+        ms7, n7 = qamr.profile_query("check_d7")
+        for k in ("check", "check_d7", "check_d6", "check1", "var", "var_init", "parity", "status", "demap"):
+            ms, n = qamr.profile_query(k)
+            if n:
+                kstats[k] = {"avg_us": 1e3 * ms / n, "launches": n, "total_ms": ms}
+        if n7:
+            bytes7, shape7 = check_class_bytes(vid, cid, 7, batch.B)
+            avg_s = ms7 / n7 / 1e3
+            ach = bytes7 / avg_s / 1e9
+            traffic = None
+            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc):
+                try:
+                    t = json.load(open(pmc))
+                    if t.get("workload") == args.workload and int(t.get("batch", -1)) == batch.B:
+                        traffic = t.get("check_d7_bytes_per_launch")
+                except Exception:
+                    traffic = None
+            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "kernel": "k_check<7,Normal> (degree-7 check-node sweep)",
+                    "bytes_per_launch": bytes7, "avg_launch_us": round(avg_s * 1e6, 1), "launches": n7}
+    # whole-decode algorithmic bandwidth (SURVEY.md 8(d) B_frame at the iterations actually run)
+    it_mean = float(its.float().mean().item())
+    V, C, E = dec.vnum, dec.cnum, dec.ednum
+    B_it = 24 * E + 24 * V + C
+    B_frame = 16 * V + C + it_mean * B_it
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        def lappr_host(n):
+            return lappr[:, :n].cpu().numpy().T.copy()
+        cpu = cpu_baseline(args, vid, cid, pipe, batch, lappr_host, args.cpu_seconds)
+
+    if rank == 0:
+        snr_, ber, fer, avg_it = SofteningPipeline.summarize(counters.cpu().numpy(), pipe.K, snr)
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (GPU-generated AWGN softening frames, torch Philox RNG)",
+            "config": {"workload": args.workload, "code": code_name, "V": V, "C": C, "E": E,
+                       "batch_per_gpu": batch.B, "global_batch": world * batch.B, "max_iterations": args.max_iter,
+                       "snr_db": snr, "bps": bps, "fused_demap": fused, "parallelism": f"dp{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "decode_alg_GBps": round(B_frame * total_frames / elapsed / 1e9, 1),
+            "mean_iterations": it_mean,
+            "ber_fer": {"ber": ber, "fer": fer, "avg_iters_success": avg_it, "frames_counted": int(counters[4])},
+            "kernels": kstats,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,226 @@
+"""ctypes facade over oracle/libqamr_oracle.so -- TEST INFRASTRUCTURE ONLY.
+
+The C restatement of the reference hot path (see qamr_oracle.c's header).  Only
+tests/, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may
+import this module; the product package (qam-reconciliation_amd/) never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libqamr_oracle.so")
+_lib = None
+
+_i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+_u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+
+
+def build() -> str:
+    """Compile the restatement (gcc -O2 -ffp-contract=off -fopenmp)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        build()
+    L = C.CDLL(_LIB_PATH)
+    vp = C.c_void_p
+    L.orc_code_create.argtypes = [_i64p, _i64p, C.c_int64, C.POINTER(vp)]
+    L.orc_code_destroy.argtypes = [vp]
+    L.orc_code_info.argtypes = [vp] + [C.POINTER(C.c_int64)] * 4
+    L.orc_box_plus.argtypes = [C.c_double, C.c_double]
+    L.orc_box_plus.restype = C.c_double
+    L.orc_check_lappr.argtypes = [vp, _f64p, _u8p]
+    L.orc_check_word.argtypes = [vp, _u8p, _u8p]
+    L.orc_check_synd_node.argtypes = [vp, C.c_int64, _u8p, _u8p]
+    L.orc_process_var_node.argtypes = [vp, C.c_int64, _f64p, _f64p, _f64p, _f64p]
+    L.orc_process_check_node.argtypes = [vp, C.c_int64, _u8p, _f64p, _f64p, _f64p]
+    L.orc_decode.argtypes = [vp, _f64p, _u8p, C.c_int, _f64p, C.POINTER(C.c_int32)]
+    L.orc_decode_batch.argtypes = [vp, C.c_int64, _f64p, _u8p, C.c_int, _f64p, _u8p, _i32p, C.c_int]
+    L.orc_eval_syndrome.argtypes = [vp, _u8p, _u8p]
+    L.orc_count_errors_from_lappr.argtypes = [_f64p, _u8p, C.c_int64]
+    L.orc_count_errors_from_lappr.restype = C.c_int64
+    L.orc_erf.argtypes = [C.c_double]
+    L.orc_erf.restype = C.c_double
+    L.orc_erf_array.argtypes = [_f64p, _f64p, C.c_int64]
+    L.orc_nm_create.argtypes = [C.c_int, C.c_double, vp, C.c_double, vp, C.POINTER(vp)]
+    L.orc_nm_destroy.argtypes = [vp]
+    L.orc_nm_tables.argtypes = [vp, _f64p, _f64p, _f64p, _f64p]
+    L.orc_single_F_Y.argtypes = [vp, C.c_double]
+    L.orc_single_F_Y.restype = C.c_double
+    L.orc_g_inv_search.argtypes = [vp, C.c_double, C.c_int, C.c_double, C.POINTER(C.c_int64)]
+    L.orc_g_inv_search.restype = C.c_double
+    L.orc_demap_lappr_array.argtypes = [vp, _f64p, _i64p, C.c_int64, _f64p, C.c_int]
+    L.orc_demap_lappr_array.restype = C.c_int64
+    L.orc_hard_decide_index.argtypes = [vp, _f64p, C.c_int64, _i64p]
+    L.orc_map_noise.argtypes = [vp, _f64p, _i64p, C.c_int64, _f64p]
+    L.orc_symbols_to_bits.argtypes = [C.c_int, _i64p, C.c_int64, _u8p]
+    _lib = L
+    return L
+
+
+class OracleCode:
+    """CPU restatement of ``qamreconciliation.Decoder`` (decoder.pyx:92-455)."""
+
+    def __init__(self, e_to_v, e_to_c):
+        vid = np.ascontiguousarray(e_to_v, dtype=np.int64)
+        cid = np.ascontiguousarray(e_to_c, dtype=np.int64)
+        if vid.size != cid.size:
+            raise ValueError("Sizes don't match")
+        h = C.c_void_p()
+        rc = lib().orc_code_create(vid, cid, vid.size, C.byref(h))
+        if rc:
+            raise ValueError(f"orc_code_create failed ({rc})")
+        self._h = h
+        v, c, e, d = (C.c_int64() for _ in range(4))
+        lib().orc_code_info(h, C.byref(v), C.byref(c), C.byref(e), C.byref(d))
+        self.vnum, self.cnum, self.ednum, self.max_dc = v.value, c.value, e.value, d.value
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _lib is not None:
+            _lib.orc_code_destroy(h)
+            self._h = None
+
+    def decode(self, lappr, synd, max_iterations):
+        lappr = np.ascontiguousarray(lappr, dtype=np.float64)
+        synd = np.ascontiguousarray(synd, dtype=np.uint8)
+        out = np.empty_like(lappr)
+        it = C.c_int32()
+        ok = lib().orc_decode(self._h, lappr, synd, int(max_iterations), out, C.byref(it))
+        return int(ok), int(it.value), out
+
+    def decode_batch(self, lappr, synd, max_iterations, nthreads=0):
+        lappr = np.ascontiguousarray(lappr, dtype=np.float64)
+        synd = np.ascontiguousarray(synd, dtype=np.uint8)
+        B = lappr.shape[0]
+        out = np.empty_like(lappr)
+        succ = np.empty(B, np.uint8)
+        its = np.empty(B, np.int32)
+        rc = lib().orc_decode_batch(self._h, B, lappr, synd, int(max_iterations), out, succ, its, int(nthreads))
+        if rc:
+            raise MemoryError("orc_decode_batch")
+        return succ, its, out
+
+    def check_lappr(self, lappr, synd):
+        return int(lib().orc_check_lappr(self._h, np.ascontiguousarray(lappr, np.float64),
+                                          np.ascontiguousarray(synd, np.uint8)))
+
+    def check_word(self, word, synd):
+        return int(lib().orc_check_word(self._h, np.ascontiguousarray(word, np.uint8),
+                                         np.ascontiguousarray(synd, np.uint8)))
+
+    def check_synd_node(self, c, word, synd):
+        return int(lib().orc_check_synd_node(self._h, int(c), np.ascontiguousarray(word, np.uint8),
+                                              np.ascontiguousarray(synd, np.uint8)))
+
+    def process_var_node(self, v, lappr, c2v, v2c, post):
+        lib().orc_process_var_node(self._h, int(v), lappr, c2v, v2c, post)
+
+    def process_check_node(self, c, synd, c2v, v2c):
+        buf = np.empty(2 * self.max_dc + 2, np.float64)
+        lib().orc_process_check_node(self._h, int(c), np.ascontiguousarray(synd, np.uint8), c2v, v2c, buf)
+
+    def eval_syndrome(self, word):
+        out = np.empty(self.cnum, np.uint8)
+        lib().orc_eval_syndrome(self._h, np.ascontiguousarray(word, np.uint8), out)
+        return out
+
+
+def box_plus(a, b):
+    return lib().orc_box_plus(float(a), float(b))
+
+
+def erf(x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    lib().orc_erf_array(x.ravel(), y.ravel(), x.size)
+    return y
+
+
+def count_errors_from_lappr(lappr, word):
+    lappr = np.ascontiguousarray(lappr, np.float64)
+    word = np.ascontiguousarray(word, np.uint8)
+    return int(lib().orc_count_errors_from_lappr(lappr, word, lappr.size))
+
+
+class OracleNoiseMapper:
+    """CPU restatement of ``PAMAlphabet`` + ``NoiseMapper`` hot-path tables and
+    ``demap_lappr_array`` (alphabet.pyx:35-76, noisemapper.pyx:103-559)."""
+
+    def __init__(self, bps, step, noise_var, sign_config=None, probabilities=None):
+        M = 1 << bps
+        self.bps, self.order = bps, M
+        self._keep = []
+        pp = None
+        if probabilities is not None:
+            p = np.ascontiguousarray(probabilities, np.float64)
+            self._keep.append(p)
+            pp = p.ctypes.data_as(C.c_void_p)
+        sp = None
+        if sign_config is not None:
+            s = np.ascontiguousarray(sign_config, np.uint8)
+            self._keep.append(s)
+            sp = s.ctypes.data_as(C.c_void_p)
+        h = C.c_void_p()
+        rc = lib().orc_nm_create(int(bps), float(step), pp, float(noise_var), sp, C.byref(h))
+        if rc:
+            raise ValueError(f"orc_nm_create failed ({rc})")
+        self._h = h
+        self.constellation = np.empty(M)
+        self.thresholds = np.empty(M + 1)
+        self.F_Y_thresholds = np.empty(M + 1)
+        self.delta_F_Y = np.empty(M)
+        lib().orc_nm_tables(h, self.constellation, self.thresholds, self.F_Y_thresholds, self.delta_F_Y)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _lib is not None:
+            _lib.orc_nm_destroy(h)
+            self._h = None
+
+    def single_F_Y(self, y):
+        return lib().orc_single_F_Y(self._h, float(y))
+
+    def g_inv_search(self, n_hat, i, y_accuracy=1e-9):
+        ev = C.c_int64(0)
+        return lib().orc_g_inv_search(self._h, float(n_hat), int(i), float(y_accuracy), C.byref(ev))
+
+    def demap_lappr_array(self, n, j, nthreads=0, return_evals=False):
+        n = np.ascontiguousarray(n, np.float64)
+        j = np.ascontiguousarray(j, np.int64)
+        if n.size != j.size:
+            raise ValueError("Sizes of transformed noise vector and tx symbols do not match")
+        out = np.empty(n.size * self.bps, np.float64)
+        ev = lib().orc_demap_lappr_array(self._h, n, j, n.size, out, int(nthreads))
+        return (out, int(ev)) if return_evals else out
+
+    def hard_decide_index(self, y):
+        y = np.ascontiguousarray(y, np.float64)
+        out = np.empty(y.size, np.int64)
+        lib().orc_hard_decide_index(self._h, y, y.size, out)
+        return out
+
+    def map_noise(self, y, xhat):
+        y = np.ascontiguousarray(y, np.float64)
+        xhat = np.ascontiguousarray(xhat, np.int64)
+        out = np.empty(y.size, np.float64)
+        lib().orc_map_noise(self._h, y, xhat, y.size, out)
+        return out
+
+    def symbols_to_bits(self, x):
+        x = np.ascontiguousarray(x, np.int64)
+        out = np.empty(x.size * self.bps, np.uint8)
+        lib().orc_symbols_to_bits(self.bps, x, x.size, out)
+        return out

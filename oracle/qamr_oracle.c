@@ -1,0 +1,469 @@
+/*
+ * qamr_oracle.c -- CPU restatement of the reference hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the HIP
+ * product path; only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it.  Nothing in qam-reconciliation_amd/ links
+ * or calls it.
+ *
+ * It restates, operation for operation, the arithmetic of
+ *   - qamreconciliation/decoder.pyx      (LDPC syndrome sum-product decoder)
+ *   - qamreconciliation/noisemapper.pyx  (softening metric / PAM soft demap)
+ *   - qamreconciliation/alphabet.pyx, bicm.pyx, matrix.pyx, utils.pyx
+ * of moriglia/qam-reconciliation.  Every function cites the reference
+ * file:line it follows.  The reference is Cython compiled by gcc -O2 for
+ * baseline x86-64 (no FMA), so this file is compiled with
+ * -O2 -ffp-contract=off and calls glibc exp/log.  scipy.special.erf (used by
+ * the reference through the Python C-API at noisemapper.pyx:66-67) is the
+ * cephes algorithm of scipy 1.15.3 (xsf/cephes/ndtr.h): it is restated in
+ * orc_erf() below and pinned bit-exactly against scipy by
+ * tests/test_oracle_golden.py.
+ *
+ * Parity pinning: see DESIGN.md "Oracle".  The restatement is checked
+ * against golden vectors produced by the reference itself (built from its
+ * own sources by oracle/Makefile into oracle/_ref/, generator script
+ * tests/golden/make_golden.py) and against the reference's own unit-test
+ * known answers (test/test_decoder.py:237-266).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORC_OK 0
+#define ORC_EVALUE 1
+#define ORC_EMEM 2
+
+/* ------------------------------------------------------------------------ */
+/* Tanner graph: decoder.pyx:93-146 (__cinit__) and :60-89 (__build_table). */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    int64_t E, V, C;
+    int64_t *chk_ptr;  /* C+1 : edges of check c are chk_edge[chk_ptr[c]..chk_ptr[c+1]) */
+    int64_t *chk_edge; /* E   : ascending edge id (scan order decoder.pyx:73-75) */
+    int64_t *var_ptr;  /* V+1 */
+    int64_t *var_edge; /* E   : ascending edge id */
+    int64_t *e_to_v;   /* E   */
+    int64_t *c_to_v;   /* E   : c_to_v[k] = e_to_v[chk_edge[k]] (decoder.pyx:128-129) */
+    int64_t max_dc;
+} orc_code;
+
+static void orc_code_free(orc_code *g) {
+    if (!g) return;
+    free(g->chk_ptr); free(g->chk_edge); free(g->var_ptr); free(g->var_edge);
+    free(g->e_to_v); free(g->c_to_v); free(g);
+}
+
+/* Stable counting sort of edge ids by node id: identical to the per-node
+ * ascending scan of __build_table (decoder.pyx:69-87) in O(E). */
+static int build_csr(const int64_t *e_to_x, int64_t E, int64_t n, int64_t **ptr_out, int64_t **edge_out) {
+    int64_t *ptr = (int64_t *)calloc((size_t)n + 1, sizeof(int64_t));
+    int64_t *edge = (int64_t *)malloc(sizeof(int64_t) * (size_t)(E > 0 ? E : 1));
+    int64_t *fill = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+    if (!ptr || !edge || !fill) { free(ptr); free(edge); free(fill); return ORC_EMEM; }
+    for (int64_t e = 0; e < E; ++e) ptr[e_to_x[e] + 1]++;
+    for (int64_t i = 0; i < n; ++i) ptr[i + 1] += ptr[i];
+    for (int64_t i = 0; i < n; ++i) fill[i] = ptr[i];
+    for (int64_t e = 0; e < E; ++e) edge[fill[e_to_x[e]]++] = e;
+    free(fill);
+    *ptr_out = ptr; *edge_out = edge;
+    return ORC_OK;
+}
+
+/* decoder.pyx:93-103: V = max(vid)+1, C = max(cid)+1; size mismatch is a
+ * ValueError (decoder.pyx:96-97).  Checks of degree < 2 are undefined
+ * behaviour in the reference (decoder.pyx:135-141, 337-342) and rejected. */
+int orc_code_create(const int64_t *e_to_v, const int64_t *e_to_c, int64_t E, orc_code **out) {
+    *out = NULL;
+    if (E <= 0) return ORC_EVALUE;
+    int64_t V = 0, C = 0;
+    for (int64_t e = 0; e < E; ++e) {
+        if (e_to_v[e] < 0 || e_to_c[e] < 0) return ORC_EVALUE;
+        if (e_to_v[e] + 1 > V) V = e_to_v[e] + 1;
+        if (e_to_c[e] + 1 > C) C = e_to_c[e] + 1;
+    }
+    orc_code *g = (orc_code *)calloc(1, sizeof(orc_code));
+    if (!g) return ORC_EMEM;
+    g->E = E; g->V = V; g->C = C;
+    if (build_csr(e_to_c, E, C, &g->chk_ptr, &g->chk_edge) ||
+        build_csr(e_to_v, E, V, &g->var_ptr, &g->var_edge)) { orc_code_free(g); return ORC_EMEM; }
+    g->e_to_v = (int64_t *)malloc(sizeof(int64_t) * (size_t)E);
+    g->c_to_v = (int64_t *)malloc(sizeof(int64_t) * (size_t)E);
+    if (!g->e_to_v || !g->c_to_v) { orc_code_free(g); return ORC_EMEM; }
+    memcpy(g->e_to_v, e_to_v, sizeof(int64_t) * (size_t)E);
+    g->max_dc = 0;
+    for (int64_t c = 0; c < C; ++c) {
+        int64_t d = g->chk_ptr[c + 1] - g->chk_ptr[c];
+        if (d < 2) { orc_code_free(g); return ORC_EVALUE; }
+        if (d > g->max_dc) g->max_dc = d;
+    }
+    for (int64_t k = 0; k < E; ++k) g->c_to_v[k] = e_to_v[g->chk_edge[k]];
+    *out = g;
+    return ORC_OK;
+}
+
+void orc_code_destroy(orc_code *g) { orc_code_free(g); }
+void orc_code_info(const orc_code *g, int64_t *V, int64_t *C, int64_t *E, int64_t *max_dc) {
+    *V = g->V; *C = g->C; *E = g->E; *max_dc = g->max_dc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Node rules.                                                              */
+/* ------------------------------------------------------------------------ */
+
+/* decoder.pyx:37-38 */
+static inline int orc_sgn(double x) { return (0.0 < x) - (x < 0.0); }
+
+/* decoder.pyx:41-45, as Cython 3 emits it: t5 = (|b| < |a|) ? |b| : |a|;
+ * r = ((sgn(a)*sgn(b)) * t5 + log(1.0 + exp(-|a+b|))) - log(1.0 + exp(-|a-b|)) */
+double orc_box_plus(double a, double b) {
+    int s = orc_sgn(a) * orc_sgn(b);
+    double fb = fabs(b), fa = fabs(a);
+    double m = (fb < fa) ? fb : fa;
+    double t1 = fabs(a + b);
+    double t2 = fabs(a - b);
+    return (((double)s * m) + log(1.0 + exp(-t1))) - log(1.0 + exp(-t2));
+}
+
+/* decoder.pyx:235-248: returns 1 iff check c is satisfied by sign(post). */
+static inline int check_lappr_node(const orc_code *g, int64_t c, const double *post, const uint8_t *synd) {
+    uint8_t parity = synd[c];
+    for (int64_t k = g->chk_ptr[c]; k < g->chk_ptr[c + 1]; ++k)
+        if (post[g->c_to_v[k]] < 0) parity ^= 1;
+    return parity ^ 1;
+}
+
+/* decoder.pyx:251-257 */
+int orc_check_lappr(const orc_code *g, const double *post, const uint8_t *synd) {
+    for (int64_t c = 0; c < g->C; ++c)
+        if (!check_lappr_node(g, c, post, synd)) return 0;
+    return 1;
+}
+
+/* decoder.pyx:177-187: word variant (parity ^= word bit). */
+int orc_check_synd_node(const orc_code *g, int64_t c, const uint8_t *word, const uint8_t *synd) {
+    uint8_t parity = synd[c];
+    for (int64_t k = g->chk_ptr[c]; k < g->chk_ptr[c + 1]; ++k) parity ^= word[g->c_to_v[k]];
+    return (uint8_t)(parity ^ 1);
+}
+
+/* decoder.pyx:212-217 */
+int orc_check_word(const orc_code *g, const uint8_t *word, const uint8_t *synd) {
+    for (int64_t c = 0; c < g->C; ++c)
+        if (!orc_check_synd_node(g, c, word, synd)) return 0;
+    return 1;
+}
+
+/* decoder.pyx:285-298 */
+void orc_process_var_node(const orc_code *g, int64_t v, const double *lappr, const double *c2v, double *v2c, double *post) {
+    int64_t b = g->var_ptr[v], e_end = g->var_ptr[v + 1];
+    post[v] = lappr[v];
+    for (int64_t k = b; k < e_end; ++k) post[v] += c2v[g->var_edge[k]];
+    for (int64_t k = b; k < e_end; ++k) v2c[g->var_edge[k]] = post[v] - c2v[g->var_edge[k]];
+}
+
+/* decoder.pyx:322-369 (F/B recursion; buf holds 2*(d-1) doubles, B = F + d - 2) */
+void orc_process_check_node(const orc_code *g, int64_t c, const uint8_t *synd, double *c2v, const double *v2c, double *buf) {
+    const int64_t *idx = g->chk_edge + g->chk_ptr[c];
+    int64_t n = g->chk_ptr[c + 1] - g->chk_ptr[c];
+    double *F = buf;
+    double *B = F + n - 2;
+    F[0] = v2c[idx[0]];
+    B[n - 1] = v2c[idx[n - 1]];
+    for (int64_t i = 1; i < n - 1; ++i) F[i] = orc_box_plus(F[i - 1], v2c[idx[i]]);
+    for (int64_t i = n - 2; i > 0; --i) B[i] = orc_box_plus(B[i + 1], v2c[idx[i]]);
+    double pre = synd[c] ? -1.0 : 1.0;
+    c2v[idx[0]] = pre * B[1];
+    for (int64_t i = 1; i < n - 1; ++i) c2v[idx[i]] = pre * orc_box_plus(F[i - 1], B[i + 1]);
+    c2v[idx[n - 1]] = pre * F[n - 2];
+}
+
+/* ------------------------------------------------------------------------ */
+/* _decode: decoder.pyx:391-436.  scratch = 2E + 2*max_dc doubles.          */
+/* ------------------------------------------------------------------------ */
+static int decode_one(const orc_code *g, const double *lappr, const uint8_t *synd, int max_it,
+                      double *final, int32_t *iters, double *scratch) {
+    if (orc_check_lappr(g, lappr, synd)) {           /* decoder.pyx:400-405 */
+        memcpy(final, lappr, sizeof(double) * (size_t)g->V);
+        *iters = 0;
+        return 1;
+    }
+    double *c2v = scratch, *v2c = scratch + g->E, *buf = scratch + 2 * g->E;
+    memset(c2v, 0, sizeof(double) * (size_t)g->E);   /* decoder.pyx:408 */
+    for (int64_t v = 0; v < g->V; ++v) orc_process_var_node(g, v, lappr, c2v, v2c, final); /* :420-421 */
+    for (int it = 0; it < max_it; ++it) {            /* :424-433 */
+        for (int64_t c = 0; c < g->C; ++c) orc_process_check_node(g, c, synd, c2v, v2c, buf);
+        for (int64_t v = 0; v < g->V; ++v) orc_process_var_node(g, v, lappr, c2v, v2c, final);
+        if (orc_check_lappr(g, final, synd)) { *iters = it + 1; return 1; }
+    }
+    *iters = max_it;                                 /* :435-436 */
+    return 0;
+}
+
+int orc_decode(const orc_code *g, const double *lappr, const uint8_t *synd, int max_it,
+               double *final, int32_t *iters) {
+    double *scratch = (double *)malloc(sizeof(double) * (size_t)(2 * g->E + 2 * g->max_dc + 2));
+    if (!scratch) return -ORC_EMEM;
+    int ok = decode_one(g, lappr, synd, max_it, final, iters, scratch);
+    free(scratch);
+    return ok;
+}
+
+/* Independent frames, frame-major [B x V] / [B x C]; OpenMP over frames
+ * (the CPU baseline of SURVEY.md 8(d)).  nthreads <= 0: library default. */
+int orc_decode_batch(const orc_code *g, int64_t B, const double *lappr, const uint8_t *synd, int max_it,
+                     double *final, uint8_t *success, int32_t *iters, int nthreads) {
+    int err = 0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+#pragma omp parallel
+    {
+        double *scratch = (double *)malloc(sizeof(double) * (size_t)(2 * g->E + 2 * g->max_dc + 2));
+        if (!scratch) {
+#pragma omp atomic write
+            err = 1;
+        } else {
+#pragma omp for schedule(dynamic, 1)
+            for (int64_t f = 0; f < B; ++f)
+                success[f] = (uint8_t)decode_one(g, lappr + f * g->V, synd + f * g->C, max_it,
+                                                 final + f * g->V, iters + f, scratch);
+            free(scratch);
+        }
+    }
+    return err ? ORC_EMEM : ORC_OK;
+}
+
+/* matrix.pyx:55-60 */
+void orc_eval_syndrome(const orc_code *g, const uint8_t *word, uint8_t *synd) {
+    memset(synd, 0, (size_t)g->C);
+    /* synd[cid[e]] ^= word[vid[e]] over all edges; XOR commutes, so the
+     * check-major walk gives the same bits as the edge-order walk. */
+    for (int64_t c = 0; c < g->C; ++c)
+        for (int64_t k = g->chk_ptr[c]; k < g->chk_ptr[c + 1]; ++k) synd[c] ^= word[g->c_to_v[k]];
+}
+
+/* utils.pyx:27-40: lappr >= 0 decides bit 0. */
+int64_t orc_count_errors_from_lappr(const double *lappr, const uint8_t *word, int64_t n) {
+    int64_t count = 0;
+    for (int64_t i = 0; i < n; ++i) count += (lappr[i] >= 0) ? word[i] : 1 - word[i];
+    return count;
+}
+
+/* ------------------------------------------------------------------------ */
+/* scipy.special.erf (scipy 1.15.3, xsf/cephes/ndtr.h erf/erfc, polevl.h).  */
+/* ------------------------------------------------------------------------ */
+static const double ndtr_P[] = {2.46196981473530512524E-10, 5.64189564831068821977E-1, 7.46321056442269912687E0,
+                                4.86371970985681366614E1,   1.96520832956077098242E2,  5.26445194995477358631E2,
+                                9.34528527171957607540E2,   1.02755188689515710272E3,  5.57535335369399327526E2};
+static const double ndtr_Q[] = {1.32281951154744992508E1, 8.67072140885989742329E1, 3.54937778887819891062E2,
+                                9.75708501743205489753E2, 1.82390916687909736289E3, 2.24633760818710981792E3,
+                                1.65666309194161350182E3, 5.57535340817727675546E2};
+static const double ndtr_R[] = {5.64189583547755073984E-1, 1.27536670759978104416E0, 5.01905042251180477414E0,
+                                6.16021097993053585195E0,  7.40974269950448939160E0, 2.97886665372100240670E0};
+static const double ndtr_S[] = {2.26052863220117276590E0, 9.39603524938001434673E0, 1.20489539808096656605E1,
+                                1.70814450747565897222E1, 9.60896809063285878198E0, 3.36907645100081516050E0};
+static const double ndtr_T[] = {9.60497373987051638749E0, 9.00260197203842689217E1, 2.23200534594684319226E3,
+                                7.00332514112805075473E3, 5.55923013010394962768E4};
+static const double ndtr_U[] = {3.35617141647503099647E1, 5.21357949780152679795E2, 4.59432382970980127987E3,
+                                2.26290000613890934246E4, 4.92673942608635921086E4};
+static const double CEPHES_MAXLOG = 7.09782712893383996732E2;
+
+static inline double polevl(double x, const double *c, int n) {
+    double ans = c[0];
+    for (int i = 1; i <= n; ++i) ans = ans * x + c[i];
+    return ans;
+}
+static inline double p1evl(double x, const double *c, int n) {
+    double ans = x + c[0];
+    for (int i = 1; i < n; ++i) ans = ans * x + c[i];
+    return ans;
+}
+
+double orc_erf(double x);
+static double orc_erfc(double a) {
+    double p, q, x, y, z;
+    if (isnan(a)) return NAN;
+    x = (a < 0.0) ? -a : a;
+    if (x < 1.0) return 1.0 - orc_erf(a);
+    z = -a * a;
+    if (z < -CEPHES_MAXLOG) goto under;
+    z = exp(z);
+    if (x < 8.0) { p = polevl(x, ndtr_P, 8); q = p1evl(x, ndtr_Q, 8); }
+    else         { p = polevl(x, ndtr_R, 5); q = p1evl(x, ndtr_S, 6); }
+    y = (z * p) / q;
+    if (a < 0) y = 2.0 - y;
+    if (y != 0.0) return y;
+under:
+    return (a < 0) ? 2.0 : 0.0;
+}
+
+double orc_erf(double x) {
+    if (isnan(x)) return NAN;
+    if (x < 0.0) return -orc_erf(-x);
+    if (fabs(x) > 1.0) return 1.0 - orc_erfc(x);
+    double z = x * x;
+    return x * polevl(z, ndtr_T, 4) / p1evl(z, ndtr_U, 5);
+}
+
+void orc_erf_array(const double *x, double *y, int64_t n) {
+    for (int64_t i = 0; i < n; ++i) y[i] = orc_erf(x[i]);
+}
+
+/* ------------------------------------------------------------------------ */
+/* PAM alphabet + NoiseMapper tables.                                       */
+/* ------------------------------------------------------------------------ */
+#define ORC_MAXM 256
+typedef struct {
+    int M, bps;
+    double a[ORC_MAXM], p[ORC_MAXM], thr[ORC_MAXM + 1];
+    double Fthr[ORC_MAXM + 1], dF[ORC_MAXM];
+    uint8_t sign[ORC_MAXM];
+    double noise_var, sigma, den; /* den = sqrt(2)*sigma (noisemapper.pyx:24,67) */
+} orc_nm;
+
+/* noisemapper.pyx:66-67 */
+static inline double F_Z(double z, double mu, double den) { return 0.5 * (1 + orc_erf((z - mu) / den)); }
+
+/* noisemapper.pyx:278-286 */
+static inline double single_F_Y(const orc_nm *nm, double y) {
+    double res = F_Z(y, nm->a[0], nm->den) * nm->p[0];
+    for (int i = 1; i < nm->M; ++i) res += F_Z(y, nm->a[i], nm->den) * nm->p[i];
+    return res;
+}
+double orc_single_F_Y(const orc_nm *nm, double y) { return single_F_Y(nm, y); }
+
+/* alphabet.pyx:35-76 (constellation :62, thresholds :69-73) and
+ * noisemapper.pyx:103-162 (sigma :132, F_Y_thresholds :149-153, delta_F_Y :159-162).
+ * probabilities == NULL -> uniform 1/M (alphabet.pyx:46-47);
+ * sign_config == NULL -> zeros (noisemapper.pyx:115-116). */
+int orc_nm_create(int bps, double step, const double *probabilities, double noise_var,
+                  const uint8_t *sign_config, orc_nm **out) {
+    *out = NULL;
+    if (bps <= 0 || bps > 8) return ORC_EVALUE;
+    if (!(noise_var > 0)) return ORC_EVALUE;
+    orc_nm *nm = (orc_nm *)calloc(1, sizeof(orc_nm));
+    if (!nm) return ORC_EMEM;
+    int M = 1 << bps;
+    nm->M = M; nm->bps = bps;
+    for (int i = 0; i < M; ++i) {
+        nm->p[i] = probabilities ? probabilities[i] : 1.0 / M;
+        nm->a[i] = ((double)i - (double)(M - 1) / 2.0) * step;
+        nm->sign[i] = sign_config ? sign_config[i] : 0;
+    }
+    for (int i = 1; i < M; ++i) nm->thr[i] = nm->a[i] - step / 2;
+    nm->thr[0] = nm->a[0] * 100;
+    nm->thr[M] = nm->a[M - 1] * 100;
+    nm->noise_var = noise_var;
+    nm->sigma = sqrt(noise_var);
+    nm->den = sqrt(2.0) * nm->sigma;
+    nm->Fthr[0] = 0;
+    nm->Fthr[M] = 1;
+    for (int i = 1; i < M; ++i) nm->Fthr[i] = single_F_Y(nm, nm->thr[i]);
+    for (int i = 0; i < M; ++i) nm->dF[i] = nm->Fthr[i + 1] - nm->Fthr[i];
+    *out = nm;
+    return ORC_OK;
+}
+void orc_nm_destroy(orc_nm *nm) { free(nm); }
+void orc_nm_tables(const orc_nm *nm, double *a, double *thr, double *Fthr, double *dF) {
+    for (int i = 0; i < nm->M; ++i) { a[i] = nm->a[i]; dF[i] = nm->dF[i]; }
+    for (int i = 0; i <= nm->M; ++i) { thr[i] = nm->thr[i]; Fthr[i] = nm->Fthr[i]; }
+}
+
+/* noisemapper.pyx:310-345 (y_accuracy default 1e-9).  *evals counts F_Y calls. */
+double orc_g_inv_search(const orc_nm *nm, double n_hat, int i, double y_accuracy, int64_t *evals) {
+    double T, F, lo, hi, mid;
+    int64_t cnt = 0;
+    if (nm->sign[i]) T = nm->Fthr[i + 1] - n_hat * nm->dF[i];
+    else             T = n_hat * nm->dF[i] + nm->Fthr[i];
+    if (T > .5) {
+        hi = 1; lo = 0;
+        F = single_F_Y(nm, hi); ++cnt;
+        while (F < T) { lo = hi; hi *= 2.; F = single_F_Y(nm, hi); ++cnt; }
+    } else {
+        lo = -1; hi = 0;
+        F = single_F_Y(nm, lo); ++cnt;
+        while (F > T) { hi = lo; lo *= 2.; F = single_F_Y(nm, lo); ++cnt; }
+    }
+    while ((hi - lo) > y_accuracy) {
+        mid = (hi + lo) / 2;
+        F = single_F_Y(nm, mid); ++cnt;
+        if (F > T) hi = mid; else lo = mid;
+    }
+    if (evals) *evals += cnt;
+    return (hi + lo) / 2;
+}
+
+/* noisemapper.pyx:450-540 */
+void orc_demap_lappr(const orc_nm *nm, double n, int64_t j, double *lappr, int64_t *evals) {
+    double N[8], D[8];
+    const double two_s2 = 2 * nm->noise_var;
+    const double *a = nm->a, *p = nm->p;
+    for (int k = 0; k < nm->bps; ++k) { N[k] = 0; D[k] = 0; }
+    for (int i = 0; i < nm->M; ++i) {
+        double y = orc_g_inv_search(nm, n, i, 1e-9, evals);
+        double s = 0;
+        for (int64_t k = 0; k < j; ++k) s += exp((2 * y - a[k] - a[j]) * (a[k] - a[j])) * p[k];
+        s += p[j];
+        for (int64_t k = j + 1; k < nm->M; ++k) s += exp((2 * y - a[k] - a[j]) * (a[k] - a[j]) / two_s2) * p[k];
+        int mi = i;
+        for (int k = 0; k < nm->bps; ++k) {
+            if ((mi * (mi + 1)) & 3) D[k] += nm->dF[i] / s;
+            else                     N[k] += nm->dF[i] / s;
+            mi >>= 1;
+        }
+    }
+    for (int k = 0; k < nm->bps; ++k) lappr[k] = log(N[k]) - log(D[k]);
+}
+
+/* noisemapper.pyx:544-559: out[s*bps + k]; OpenMP over symbols. Returns the
+ * total number of F_Y evaluations (the demap cost driver). */
+int64_t orc_demap_lappr_array(const orc_nm *nm, const double *n, const int64_t *j, int64_t S, double *lappr, int nthreads) {
+    int64_t evals = 0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+#pragma omp parallel for schedule(dynamic, 64) reduction(+ : evals)
+    for (int64_t s = 0; s < S; ++s) {
+        int64_t ev = 0;
+        orc_demap_lappr(nm, n[s], j[s], lappr + s * nm->bps, &ev);
+        evals += ev;
+    }
+    return evals;
+}
+
+/* Bob side (next-row inputs): noisemapper.pyx:27-44 (__binsearch),
+ * :349-359 (hard_decide_index), :289-292 (g), :373-388 (map_noise). */
+static int64_t binsearch(const double *dom, int64_t size, double val) {
+    if (size == 1) return 0;
+    if (val < dom[0]) return 0;
+    if (val > dom[size - 1]) return size - 1;
+    int64_t index = size / 2 - 1;
+    if (val < dom[index]) return binsearch(dom, index, val);
+    if (val >= dom[index + 1]) return index + 1 + binsearch(dom + index + 1, size - index - 1, val);
+    return index;
+}
+void orc_hard_decide_index(const orc_nm *nm, const double *y, int64_t S, int64_t *xhat) {
+    for (int64_t s = 0; s < S; ++s) {
+        int64_t r = binsearch(nm->thr, nm->M + 1, y[s]);
+        if (r == nm->M) r = nm->M - 1;
+        xhat[s] = r;
+    }
+}
+double orc_g(const orc_nm *nm, double y, int i) {
+    if (nm->sign[i]) return (nm->Fthr[i + 1] - single_F_Y(nm, y)) / nm->dF[i];
+    return (single_F_Y(nm, y) - nm->Fthr[i]) / nm->dF[i];
+}
+void orc_map_noise(const orc_nm *nm, const double *y, const int64_t *xhat, int64_t S, double *n) {
+    for (int64_t s = 0; s < S; ++s) n[s] = orc_g(nm, y[s], (int)xhat[s]);
+}
+/* alphabet.pyx:98-107 with the reflected Gray table of bicm.pyx:26-41 */
+void orc_symbols_to_bits(int bps, const int64_t *x, int64_t S, uint8_t *bits) {
+    for (int64_t s = 0; s < S; ++s) {
+        int64_t g = x[s] ^ (x[s] >> 1);
+        for (int k = 0; k < bps; ++k) bits[s * bps + k] = (uint8_t)((g >> k) & 1);
+    }
+}

@@ -1,0 +1,327 @@
+// demap.hip -- PAM/BICM soft demapper (Alice side of the softening scheme) and
+// the Bob-side producers of its inputs, for gfx950.
+//
+// Reference: qamreconciliation/noisemapper.pyx (NoiseMapper), alphabet.pyx,
+// bicm.pyx, matrix.pyx, utils.pyx, sims/reconciliation.pyx:93-168.
+//
+// One lane = one (symbol, frame).  The lane runs the reference's per-symbol
+// procedure (noisemapper.pyx:450-540) sequentially: for each hypothesis i a
+// bracket + bisection inversion of the mixture CDF F_Y (31..40 F_Y
+// evaluations of M scipy-exact erf each), then the Gray-labelled N/D sums in
+// i order.  This is fp64-VALU bound (bytes are negligible); lanes of a wave
+// hold 64 consecutive frames of the same symbol position so the LAPPR stores
+// land directly, coalesced, in the decoder's frame-innermost input layout.
+#include <vector>
+
+#include "qamr_internal.hpp"
+
+namespace qr {
+
+__global__ void __launch_bounds__(256) k_demap(const DemapTables *__restrict__ tab, int B, int ld, int64_t S,
+                                               const double *__restrict__ n, const int64_t *__restrict__ j,
+                                               double alpha, double *__restrict__ lappr) {
+    const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t s = item / ld;
+    const int f = (int)(item - s * ld);
+    if (s >= S || f >= B) return;
+    const DemapTables &t = *tab;
+    const double nv = n[s * ld + f];
+    const int64_t jv = j[s * ld + f];
+    double out[kMaxBps];
+    if (jv < 0 || jv >= t.M) {
+#pragma unroll
+        for (int k = 0; k < kMaxBps; ++k) out[k] = __builtin_nan("");
+    } else {
+        demap_symbol(t, nv, (int)jv, alpha, out);
+    }
+    const int bps = t.bps;
+#pragma unroll
+    for (int k = 0; k < kMaxBps; ++k)
+        if (k < bps) lappr[(s * bps + k) * ld + f] = out[k];
+}
+
+// Bob: hard decision (noisemapper.pyx:349-359), transformed noise g(y, x_hat)
+// (:289-292, :373-388) and Gray bits of x_hat (alphabet.pyx:98-107, bicm.pyx:26-41).
+__global__ void __launch_bounds__(256) k_bob(const DemapTables *__restrict__ tab, int B, int ld, int64_t S,
+                                             const double *__restrict__ y, int64_t *__restrict__ xhat,
+                                             double *__restrict__ nhat, uint8_t *__restrict__ word) {
+    const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t s = item / ld;
+    const int f = (int)(item - s * ld);
+    if (s >= S || f >= B) return;
+    const DemapTables &t = *tab;
+    const double yv = y[s * ld + f];
+    int i = binsearch_thr(t.thr, t.M + 1, yv);
+    if (i == t.M) i = t.M - 1;
+    double g;
+    if (t.sign[i]) g = (t.Fthr[i + 1] - single_F_Y(t, yv)) / t.dF[i];
+    else           g = (single_F_Y(t, yv) - t.Fthr[i]) / t.dF[i];
+    xhat[s * ld + f] = i;
+    nhat[s * ld + f] = g;
+    const int gray = i ^ (i >> 1);
+    for (int k = 0; k < t.bps; ++k) word[(s * t.bps + k) * ld + f] = (uint8_t)((gray >> k) & 1);
+}
+
+// noisemapper.pyx:289-292, :373-388 with a caller-given index (x_hat).
+__global__ void __launch_bounds__(256) k_map_noise(const DemapTables *__restrict__ tab, int B, int ld, int64_t S,
+                                                   const double *__restrict__ y, const int64_t *__restrict__ idx,
+                                                   double *__restrict__ nhat) {
+    const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t s = item / ld;
+    const int f = (int)(item - s * ld);
+    if (s >= S || f >= B) return;
+    const DemapTables &t = *tab;
+    const double yv = y[s * ld + f];
+    const int64_t i = idx[s * ld + f];
+    double g;
+    if (i < 0 || i >= t.M) g = __builtin_nan("");
+    else if (t.sign[i]) g = (t.Fthr[i + 1] - single_F_Y(t, yv)) / t.dF[i];
+    else g = (single_F_Y(t, yv) - t.Fthr[i]) / t.dF[i];
+    nhat[s * ld + f] = g;
+}
+
+// matrix.pyx:55-60, frame-innermost; one lane = (check, frame).
+__global__ void __launch_bounds__(256) k_syndrome(int64_t C, int ld, int B, const int32_t *__restrict__ chk_ptr,
+                                                  const int32_t *__restrict__ chk_var,
+                                                  const uint8_t *__restrict__ word, uint8_t *__restrict__ synd) {
+    const int f = blockIdx.y * blockDim.x + threadIdx.x;
+    const int64_t c = blockIdx.x;
+    if (c >= C || f >= ld) return;
+    uint8_t x = 0;
+    if (f < B)
+        for (int k = chk_ptr[c]; k < chk_ptr[c + 1]; ++k) x ^= word[(size_t)chk_var[k] * ld + f];
+    synd[(size_t)c * ld + f] = x;
+}
+
+// utils.pyx:27-40 (lappr >= 0 decides bit 0) over the first K nodes, then the
+// per-frame bookkeeping of reconciliation.pyx:149-157.
+__global__ void __launch_bounds__(256) k_count_errors(int B, int ld, int64_t K, int64_t kpb,
+                                                      const double *__restrict__ fin,
+                                                      const uint8_t *__restrict__ word, int32_t *__restrict__ ferr) {
+    const int f = blockIdx.y * blockDim.x + threadIdx.x;
+    if (f >= B) return;
+    const int64_t v0 = (int64_t)blockIdx.x * kpb;
+    const int64_t v1 = (v0 + kpb < K) ? v0 + kpb : K;
+    int32_t cnt = 0;
+    for (int64_t v = v0; v < v1; ++v) {
+        const uint8_t w = word[v * ld + f];
+        cnt += (fin[v * ld + f] >= 0) ? w : 1 - w;
+    }
+    if (cnt) atomicAdd(&ferr[f], cnt);
+}
+
+__global__ void k_count_finish(int B, const int32_t *__restrict__ ferr, const uint8_t *__restrict__ success,
+                               const int32_t *__restrict__ iters, unsigned long long *counters) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long be = 0, fe = 0, su = 0, it = 0, fr = 0;
+    if (f < B) {
+        be = (unsigned long long)ferr[f];
+        fe = ferr[f] ? 1 : 0;
+        su = success[f] ? 1 : 0;
+        it = success[f] ? (unsigned long long)iters[f] : 0;
+        fr = 1;
+    }
+    // wave-level sums, then one atomic per wave per counter
+    for (int off = 32; off > 0; off >>= 1) {
+        be += __shfl_down(be, off);
+        fe += __shfl_down(fe, off);
+        su += __shfl_down(su, off);
+        it += __shfl_down(it, off);
+        fr += __shfl_down(fr, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&counters[0], be);
+        atomicAdd(&counters[1], fe);
+        atomicAdd(&counters[2], su);
+        atomicAdd(&counters[3], it);
+        atomicAdd(&counters[4], fr);
+    }
+}
+
+static int check_shape(int B, int ld, int64_t S) {
+    if (B <= 0 || ld < B || ld % kWave) return set_error(QR_EVALUE, "need 0 < B <= ld, ld %% 64 == 0 (B=%d ld=%d)", B, ld);
+    if (S <= 0) return set_error(QR_EVALUE, "S must be positive");
+    return QR_OK;
+}
+
+int demap_batch_device(const qr_demap *dm, int B, int ld, int64_t S, const double *n, const int64_t *j, double alpha,
+                       double *lappr, hipStream_t s) {
+    int rc = check_shape(B, ld, S);
+    if (rc) return rc;
+    DeviceGuard g(dm->device);
+    ProfScope ps("demap", s);
+    const int64_t items = S * ld;
+    k_demap<<<(unsigned)((items + 255) / 256), 256, 0, s>>>(dm->d_tables, B, ld, S, n, j, alpha, lappr);
+    QR_LAUNCH_CHECK();
+    return QR_OK;
+}
+
+}  // namespace qr
+
+// ===================================================================== C-ABI
+using namespace qr;
+
+extern "C" {
+
+int qr_demap_create(int32_t bps, const double *constellation, const double *probabilities, const double *thresholds,
+                    double noise_var, const uint8_t *sign_config, int32_t device, qr_demap **out) {
+    if (!out) return set_error(QR_EVALUE, "null output handle");
+    *out = nullptr;
+    if (bps < 1 || bps > kMaxBps) return set_error(QR_EVALUE, "bit_per_symbol must be in [1, %d], got %d", kMaxBps, bps);
+    // noisemapper.pyx:111-112
+    if (!(noise_var > 0)) return set_error(QR_EVALUE, "noise variance must be strictly positive, got %g", noise_var);
+    if (!constellation || !thresholds) return set_error(QR_EVALUE, "null constellation/thresholds");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return set_error(QR_EDEVICE, "no HIP device available (libqamr has no CPU fallback)");
+    if (device < 0 || device >= ndev) return set_error(QR_EVALUE, "device %d out of range", device);
+    qr_demap *dm = new qr_demap();
+    DemapTables &t = dm->h;
+    memset(&t, 0, sizeof t);
+    const int M = 1 << bps;
+    t.M = M;
+    t.bps = bps;
+    for (int i = 0; i < M; ++i) {
+        t.a[i] = constellation[i];
+        t.p[i] = probabilities ? probabilities[i] : 1.0 / M;  // alphabet.pyx:46-47
+        t.sign[i] = sign_config ? sign_config[i] : 0;       // noisemapper.pyx:115-116
+    }
+    for (int i = 0; i <= M; ++i) t.thr[i] = thresholds[i];
+    const double sigma = sqrt(noise_var);                     // noisemapper.pyx:132
+    t.den = sqrt(2.0) * sigma;                                // __sqrt2 * sigma (:24, :67)
+    t.two_s2 = 2 * noise_var;                                 // :469
+    t.Fthr[0] = 0;                                            // :149-153
+    t.Fthr[M] = 1;
+    for (int i = 1; i < M; ++i) t.Fthr[i] = single_F_Y(t, t.thr[i]);
+    for (int i = 0; i < M; ++i) t.dF[i] = t.Fthr[i + 1] - t.Fthr[i];  // :159-162
+    dm->device = device;
+    dm->scratch.device = device;
+    DeviceGuard g(device);
+    hipError_t e = hipMalloc((void **)&dm->d_tables, sizeof(DemapTables));
+    if (e == hipSuccess) e = hipMemcpy(dm->d_tables, &t, sizeof(DemapTables), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (dm->d_tables) (void)hipFree(dm->d_tables);
+        delete dm;
+        return hip_fail(e, "qr_demap_create upload", __FILE__, __LINE__);
+    }
+    *out = dm;
+    return QR_OK;
+}
+
+int qr_demap_destroy(qr_demap *dm) {
+    if (!dm) return QR_OK;
+    {
+        DeviceGuard g(dm->device);
+        (void)hipFree(dm->d_tables);
+    }
+    delete dm;
+    return QR_OK;
+}
+
+int qr_demap_tables(const qr_demap *dm, double *Fthr, double *dF) {
+    if (!dm) return set_error(QR_EVALUE, "null demapper");
+    for (int i = 0; i <= dm->h.M; ++i)
+        if (Fthr) Fthr[i] = dm->h.Fthr[i];
+    for (int i = 0; i < dm->h.M; ++i)
+        if (dF) dF[i] = dm->h.dF[i];
+    return QR_OK;
+}
+
+int qr_demap_batch_device(const qr_demap *dm, int32_t B, int32_t ld, int64_t S, const double *d_n,
+                          const int64_t *d_j, double alpha, double *d_lappr, void *stream) {
+    if (!dm) return set_error(QR_EVALUE, "null demapper");
+    return demap_batch_device(dm, B, ld, S, d_n, d_j, alpha, d_lappr, (hipStream_t)stream);
+}
+
+// One array from host memory: the same kernel with B = ld = 1, i.e. one lane
+// per symbol and the interleaved out[s*bps + k] layout of noisemapper.pyx:556.
+int qr_demap_host(const qr_demap *dm, int64_t S, const double *n, const int64_t *j, double *lappr) {
+    if (!dm) return set_error(QR_EVALUE, "null demapper");
+    if (S <= 0) return QR_OK;
+    DeviceGuard g(dm->device);
+    std::lock_guard<std::mutex> lk(dm->scratch.mu);
+    const int bps = dm->h.bps;
+    const size_t a = align_up(S * 8, 256), b = align_up(S * 8, 256), c = align_up(S * bps * 8, 256);
+    int rc = dm->scratch.reserve(a + b + c);
+    if (rc) return rc;
+    char *p = (char *)dm->scratch.ptr;
+    double *d_n = (double *)p;
+    int64_t *d_j = (int64_t *)(p + a);
+    double *d_l = (double *)(p + a + b);
+    QR_HIP(hipMemcpy(d_n, n, S * 8, hipMemcpyHostToDevice));
+    QR_HIP(hipMemcpy(d_j, j, S * 8, hipMemcpyHostToDevice));
+    // ld = 1, B = 1: item = s, f = 0; lappr index (s*bps + k) * 1 + 0 = interleaved output.
+    {
+        ProfScope ps("demap", nullptr);
+        k_demap<<<(unsigned)((S + 255) / 256), 256>>>(dm->d_tables, 1, 1, S, d_n, d_j, 1.0, d_l);
+        QR_LAUNCH_CHECK();
+    }
+    QR_HIP(hipMemcpy(lappr, d_l, S * bps * 8, hipMemcpyDeviceToHost));
+    return QR_OK;
+}
+
+int qr_bob_map_device(const qr_demap *dm, int32_t B, int32_t ld, int64_t S, const double *d_y, int64_t *d_xhat,
+                      double *d_nhat, uint8_t *d_word, void *stream) {
+    if (!dm) return set_error(QR_EVALUE, "null demapper");
+    int rc = check_shape(B, ld, S);
+    if (rc) return rc;
+    DeviceGuard g(dm->device);
+    hipStream_t s = (hipStream_t)stream;
+    ProfScope ps("bob", s);
+    const int64_t items = S * ld;
+    k_bob<<<(unsigned)((items + 255) / 256), 256, 0, s>>>(dm->d_tables, B, ld, S, d_y, d_xhat, d_nhat, d_word);
+    QR_LAUNCH_CHECK();
+    return QR_OK;
+}
+
+int qr_map_noise_device(const qr_demap *dm, int32_t B, int32_t ld, int64_t S, const double *d_y,
+                        const int64_t *d_index, double *d_nhat, void *stream) {
+    if (!dm) return set_error(QR_EVALUE, "null demapper");
+    int rc = check_shape(B, ld, S);
+    if (rc) return rc;
+    DeviceGuard g(dm->device);
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t items = S * ld;
+    k_map_noise<<<(unsigned)((items + 255) / 256), 256, 0, s>>>(dm->d_tables, B, ld, S, d_y, d_index, d_nhat);
+    QR_LAUNCH_CHECK();
+    return QR_OK;
+}
+
+int qr_syndrome_device(const qr_code *code, int32_t B, int32_t ld, const uint8_t *d_word, uint8_t *d_synd,
+                       void *stream) {
+    if (!code) return set_error(QR_EVALUE, "null code");
+    int rc = check_shape(B, ld, 1);
+    if (rc) return rc;
+    DeviceGuard g(code->device);
+    hipStream_t s = (hipStream_t)stream;
+    ProfScope ps("syndrome", s);
+    const int ft = frame_tile(ld);
+    dim3 grid((unsigned)code->C, (unsigned)(ld / ft));
+    k_syndrome<<<grid, ft, 0, s>>>(code->C, ld, B, code->d_chk_ptr, code->d_chk_var, d_word, d_synd);
+    QR_LAUNCH_CHECK();
+    return QR_OK;
+}
+
+int qr_count_errors_device(int32_t B, int32_t ld, int64_t K, const double *d_final, const uint8_t *d_word,
+                           const uint8_t *d_success, const int32_t *d_iters, int32_t *d_frame_errors,
+                           int64_t *d_counters, void *stream) {
+    int rc = check_shape(B, ld, 1);
+    if (rc) return rc;
+    if (K < 0) return set_error(QR_EVALUE, "K must be >= 0");
+    hipStream_t s = (hipStream_t)stream;
+    ProfScope ps("count", s);
+    int32_t *ferr = d_frame_errors;
+    QR_HIP(hipMemsetAsync(ferr, 0, (size_t)B * 4, s));
+    if (K > 0) {
+        const int ft = frame_tile(ld);
+        const int64_t kpb = 64;
+        dim3 grid((unsigned)((K + kpb - 1) / kpb), (unsigned)(ld / ft));
+        k_count_errors<<<grid, ft, 0, s>>>(B, ld, K, kpb, d_final, d_word, ferr);
+        QR_LAUNCH_CHECK();
+    }
+    k_count_finish<<<(B + 255) / 256, 256, 0, s>>>(B, ferr, d_success, d_iters, (unsigned long long *)d_counters);
+    QR_LAUNCH_CHECK();
+    return QR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,97 @@
+// qamr_internal.hpp -- shared host-side definitions of libqamr.so.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "qamr.h"
+#include "qamr_math.hpp"
+
+namespace qr {
+
+// ------------------------------------------------------------------ errors
+int set_error(int code, const char *fmt, ...);
+int hip_fail(hipError_t e, const char *what, const char *file, int line);
+
+#define QR_HIP(call)                                                            \
+    do {                                                                        \
+        hipError_t _qr_e = (call);                                              \
+        if (_qr_e != hipSuccess) return ::qr::hip_fail(_qr_e, #call, __FILE__, __LINE__); \
+    } while (0)
+
+#define QR_LAUNCH_CHECK() QR_HIP(hipGetLastError())
+
+// --------------------------------------------------------------- profiling
+// hipEvent pair recorded on the launch stream around one kernel launch.
+struct ProfScope {
+    ProfScope(std::string name, hipStream_t s);
+    ~ProfScope();
+    std::string name_;
+    hipStream_t s_;
+    hipEvent_t a_ = nullptr, b_ = nullptr;
+};
+bool profiling_on();
+
+// ------------------------------------------------------------------ layout
+constexpr int kWave = 64;
+inline int frame_tile(int ld) { return (ld % 256 == 0) ? 256 : (ld % 128 == 0) ? 128 : 64; }
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Device scratch owned by a handle, grown on demand (host-API calls only).
+struct Scratch {
+    std::mutex mu;
+    void *ptr = nullptr;
+    size_t bytes = 0;
+    int device = 0;
+    int reserve(size_t want);  // caller holds mu
+    ~Scratch();
+};
+
+// Kernel launchers shared between translation units.
+int launch_transpose_to_fi_f64(int B, int ld, int64_t n, const double *src, double *dst, hipStream_t s);
+int launch_transpose_to_fm_f64(int B, int ld, int64_t n, const double *src, double *dst, hipStream_t s);
+int launch_transpose_to_fi_u8(int B, int ld, int64_t n, const uint8_t *src, uint8_t *dst, hipStream_t s);
+int launch_transpose_to_fi_i64(int B, int ld, int64_t n, const int64_t *src, int64_t *dst, hipStream_t s);
+
+struct DeviceGuard {
+    explicit DeviceGuard(int dev) {
+        (void)hipGetDevice(&prev_);
+        if (prev_ != dev) (void)hipSetDevice(dev);
+        dev_ = dev;
+    }
+    ~DeviceGuard() {
+        if (prev_ != dev_) (void)hipSetDevice(prev_);
+    }
+    int prev_ = 0, dev_ = 0;
+};
+
+}  // namespace qr
+
+// --------------------------------------------------------------- handles
+struct DegreeClass {
+    int32_t degree;
+    int64_t n;
+    int32_t *d_checks;  // check ids of this degree, ascending
+};
+
+struct qr_code {
+    int64_t E = 0, V = 0, C = 0;
+    int32_t max_dc = 0, max_dv = 0;
+    int device = 0;
+    // CSR, int32 (E < 2^31): per check, edge ids ascending and their variables;
+    // per variable, edge ids ascending.
+    int32_t *d_chk_ptr = nullptr, *d_chk_edge = nullptr, *d_chk_var = nullptr;
+    int32_t *d_var_ptr = nullptr, *d_var_edge = nullptr;
+    std::vector<DegreeClass> classes;
+    mutable qr::Scratch scratch;
+};
+
+struct qr_demap {
+    int device = 0;
+    qr::DemapTables h;                      // host copy
+    qr::DemapTables *d_tables = nullptr;    // device copy
+    mutable qr::Scratch scratch;
+};

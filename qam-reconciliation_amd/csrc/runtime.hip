@@ -1,0 +1,232 @@
+// runtime.hip -- error reporting, per-kernel event timing, device scratch and
+// the frame-major <-> frame-innermost transposes of libqamr.so.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include <atomic>
+#include <map>
+
+#include "qamr_internal.hpp"
+
+namespace qr {
+
+static thread_local std::string g_err;
+
+int set_error(int code, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *what, const char *file, int line) {
+    if (e == hipErrorOutOfMemory)
+        return set_error(QR_EMEMORY, "out of device memory in %s (%s:%d)", what, file, line);
+    return set_error(QR_EDEVICE, "HIP error %d (%s) in %s (%s:%d)", (int)e, hipGetErrorString(e), what, file, line);
+}
+
+// ------------------------------------------------------------------ profiling
+namespace {
+struct Pending {
+    std::string name;
+    hipEvent_t a, b;
+};
+struct Stat {
+    double ms = 0;
+    int64_t n = 0;
+};
+std::atomic<bool> g_prof{false};
+std::mutex g_prof_mu;
+std::vector<Pending> g_pending;
+std::map<std::string, Stat> g_stats;
+
+void drain_pending_locked() {
+    for (auto &p : g_pending) {
+        float ms = 0.f;
+        if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            auto &s = g_stats[p.name];
+            s.ms += ms;
+            s.n += 1;
+        }
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    g_pending.clear();
+}
+}  // namespace
+
+bool profiling_on() { return g_prof.load(std::memory_order_relaxed); }
+
+ProfScope::ProfScope(std::string name, hipStream_t s) : name_(std::move(name)), s_(s) {
+    if (!profiling_on()) return;
+    if (hipEventCreate(&a_) != hipSuccess || hipEventCreate(&b_) != hipSuccess) {
+        a_ = b_ = nullptr;
+        return;
+    }
+    (void)hipEventRecord(a_, s_);
+}
+
+ProfScope::~ProfScope() {
+    if (!a_) return;
+    (void)hipEventRecord(b_, s_);
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_pending.push_back({name_, a_, b_});
+    if (g_pending.size() > 4096) drain_pending_locked();
+}
+
+// ------------------------------------------------------------------ scratch
+int Scratch::reserve(size_t want) {
+    if (want <= bytes) return QR_OK;
+    if (ptr) {
+        (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+    QR_HIP(hipMalloc(&ptr, want));
+    bytes = want;
+    return QR_OK;
+}
+
+Scratch::~Scratch() {
+    if (ptr) {
+        DeviceGuard g(device);
+        (void)hipFree(ptr);
+    }
+}
+
+// ---------------------------------------------------------------- transposes
+// Frame-major src[f * n + i] (f < B)  ->  frame-innermost dst[i * ld + f].
+// 64x64 tiles staged through LDS (padded by one element against bank
+// conflicts); 256 threads = 4 waves, each lane moves 16 elements.
+template <typename T>
+__global__ void __launch_bounds__(256) k_to_fi(int B, int ld, int64_t n, const T *__restrict__ src, T *__restrict__ dst) {
+    __shared__ T tile[64][65];
+    const int64_t i0 = (int64_t)blockIdx.x * 64;
+    const int f0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int f = f0 + ty * 16 + r;
+        const int64_t i = i0 + tx;
+        tile[ty * 16 + r][tx] = (f < B && i < n) ? src[(int64_t)f * n + i] : T(0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t i = i0 + ty * 16 + r;
+        const int f = f0 + tx;
+        if (i < n && f < ld) dst[i * ld + f] = tile[tx][ty * 16 + r];
+    }
+}
+
+// Frame-innermost src[i * ld + f] -> frame-major dst[f * n + i] (f < B).
+template <typename T>
+__global__ void __launch_bounds__(256) k_to_fm(int B, int ld, int64_t n, const T *__restrict__ src, T *__restrict__ dst) {
+    __shared__ T tile[64][65];
+    const int64_t i0 = (int64_t)blockIdx.x * 64;
+    const int f0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t i = i0 + ty * 16 + r;
+        const int f = f0 + tx;
+        tile[ty * 16 + r][tx] = (i < n && f < B) ? src[i * ld + f] : T(0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int f = f0 + ty * 16 + r;
+        const int64_t i = i0 + tx;
+        if (f < B && i < n) dst[(int64_t)f * n + i] = tile[tx][ty * 16 + r];
+    }
+}
+
+template <typename T>
+static int launch_to_fi(int B, int ld, int64_t n, const T *src, T *dst, hipStream_t s) {
+    if (B <= 0 || ld < B || ld % kWave || n <= 0) return set_error(QR_EVALUE, "bad transpose shape B=%d ld=%d n=%lld", B, ld, (long long)n);
+    dim3 grid((unsigned)((n + 63) / 64), (unsigned)((ld + 63) / 64));
+    k_to_fi<T><<<grid, 256, 0, s>>>(B, ld, n, src, dst);
+    QR_LAUNCH_CHECK();
+    return QR_OK;
+}
+template <typename T>
+static int launch_to_fm(int B, int ld, int64_t n, const T *src, T *dst, hipStream_t s) {
+    if (B <= 0 || ld < B || ld % kWave || n <= 0) return set_error(QR_EVALUE, "bad transpose shape B=%d ld=%d n=%lld", B, ld, (long long)n);
+    dim3 grid((unsigned)((n + 63) / 64), (unsigned)((B + 63) / 64));
+    k_to_fm<T><<<grid, 256, 0, s>>>(B, ld, n, src, dst);
+    QR_LAUNCH_CHECK();
+    return QR_OK;
+}
+
+int launch_transpose_to_fi_f64(int B, int ld, int64_t n, const double *src, double *dst, hipStream_t s) {
+    return launch_to_fi<double>(B, ld, n, src, dst, s);
+}
+int launch_transpose_to_fm_f64(int B, int ld, int64_t n, const double *src, double *dst, hipStream_t s) {
+    return launch_to_fm<double>(B, ld, n, src, dst, s);
+}
+int launch_transpose_to_fi_u8(int B, int ld, int64_t n, const uint8_t *src, uint8_t *dst, hipStream_t s) {
+    return launch_to_fi<uint8_t>(B, ld, n, src, dst, s);
+}
+int launch_transpose_to_fi_i64(int B, int ld, int64_t n, const int64_t *src, int64_t *dst, hipStream_t s) {
+    return launch_to_fi<int64_t>(B, ld, n, src, dst, s);
+}
+
+}  // namespace qr
+
+// ===================================================================== C-ABI
+extern "C" {
+
+const char *qr_last_error(void) { return qr::g_err.c_str(); }
+
+int qr_version(int32_t *major, int32_t *minor) {
+    if (major) *major = 0;
+    if (minor) *minor = 1;
+    return QR_OK;
+}
+
+int qr_device_count(int32_t *count) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *count = n;
+    return QR_OK;
+}
+
+int qr_profile_enable(int32_t on) {
+    qr::g_prof.store(on != 0);
+    return QR_OK;
+}
+
+int qr_profile_reset(void) {
+    std::lock_guard<std::mutex> lk(qr::g_prof_mu);
+    qr::drain_pending_locked();
+    qr::g_stats.clear();
+    return QR_OK;
+}
+
+int qr_profile_query(const char *name, double *total_ms, int64_t *launches) {
+    std::lock_guard<std::mutex> lk(qr::g_prof_mu);
+    qr::drain_pending_locked();
+    auto it = qr::g_stats.find(name ? name : "");
+    *total_ms = (it == qr::g_stats.end()) ? 0.0 : it->second.ms;
+    *launches = (it == qr::g_stats.end()) ? 0 : it->second.n;
+    return QR_OK;
+}
+
+int qr_to_frame_innermost_f64(int32_t B, int32_t ld, int64_t n, const double *s, double *d, void *st) {
+    return qr::launch_transpose_to_fi_f64(B, ld, n, s, d, (hipStream_t)st);
+}
+int qr_to_frame_major_f64(int32_t B, int32_t ld, int64_t n, const double *s, double *d, void *st) {
+    return qr::launch_transpose_to_fm_f64(B, ld, n, s, d, (hipStream_t)st);
+}
+int qr_to_frame_innermost_u8(int32_t B, int32_t ld, int64_t n, const uint8_t *s, uint8_t *d, void *st) {
+    return qr::launch_transpose_to_fi_u8(B, ld, n, s, d, (hipStream_t)st);
+}
+int qr_to_frame_innermost_i64(int32_t B, int32_t ld, int64_t n, const int64_t *s, int64_t *d, void *st) {
+    return qr::launch_transpose_to_fi_i64(B, ld, n, s, d, (hipStream_t)st);
+}
+
+}  // extern "C"

@@ -1,0 +1,134 @@
+"""ctypes binding of libqamr.so (declared in include/qamr.h).
+
+There is no CPU fallback: if the library or a HIP device is missing, every
+compute entry point raises.  ``load()`` only needs the shared object (it works
+on a CPU-only host, for symbol checks).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libqamr.so")
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+
+QR_OK, QR_EVALUE, QR_EMEMORY, QR_EDEVICE, QR_EUNSUPPORTED = 0, 1, 2, 3, 4
+
+_lib = None
+
+vp = C.c_void_p
+i32, i64, f64, u8 = C.c_int32, C.c_int64, C.c_double, C.c_uint8
+P = C.POINTER
+
+# name -> (argtypes); restype is int unless listed in _RESTYPE.
+SIGNATURES = {
+    "qr_last_error": [],
+    "qr_version": [P(i32), P(i32)],
+    "qr_device_count": [P(i32)],
+    "qr_profile_enable": [i32],
+    "qr_profile_reset": [],
+    "qr_profile_query": [C.c_char_p, P(f64), P(i64)],
+    "qr_code_create": [vp, vp, i64, i64, i32, P(vp)],
+    "qr_code_destroy": [vp],
+    "qr_code_info": [vp, P(i64), P(i64), P(i64), P(i32), P(i32)],
+    "qr_decode_workspace_size": [vp, i32, i32, P(C.c_size_t)],
+    "qr_decode_batch_device": [vp, i32, i32, vp, vp, i32, vp, vp, vp, vp, C.c_size_t, vp],
+    "qr_decode_host": [vp, i32, vp, vp, i32, vp, vp, vp],
+    "qr_check_lappr_host": [vp, vp, vp, vp, vp],
+    "qr_check_word_host": [vp, vp, vp, vp, vp],
+    "qr_process_var_nodes_host": [vp, vp, i64, vp, vp, vp, vp],
+    "qr_process_check_nodes_host": [vp, vp, i64, vp, vp, vp],
+    "qr_demap_create": [i32, vp, vp, vp, f64, vp, i32, P(vp)],
+    "qr_demap_destroy": [vp],
+    "qr_demap_tables": [vp, vp, vp],
+    "qr_demap_batch_device": [vp, i32, i32, i64, vp, vp, f64, vp, vp],
+    "qr_demap_host": [vp, i64, vp, vp, vp],
+    "qr_bob_map_device": [vp, i32, i32, i64, vp, vp, vp, vp, vp],
+    "qr_map_noise_device": [vp, i32, i32, i64, vp, vp, vp, vp],
+    "qr_syndrome_device": [vp, i32, i32, vp, vp, vp],
+    "qr_count_errors_device": [i32, i32, i64, vp, vp, vp, vp, vp, vp, vp],
+    "qr_to_frame_innermost_f64": [i32, i32, i64, vp, vp, vp],
+    "qr_to_frame_major_f64": [i32, i32, i64, vp, vp, vp],
+    "qr_to_frame_innermost_u8": [i32, i32, i64, vp, vp, vp],
+    "qr_to_frame_innermost_i64": [i32, i32, i64, vp, vp, vp],
+}
+_RESTYPE = {"qr_last_error": C.c_char_p}
+
+
+class QamrError(RuntimeError):
+    pass
+
+
+def build(verbose: bool = False) -> str:
+    """Compile libqamr.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    jobs = min(3, os.cpu_count() or 1)
+    subprocess.run(["make", "-s" if not verbose else "-w", f"-j{jobs}", "-C", CSRC], check=True)
+    return LIB_PATH
+
+
+def load():
+    """Load the shared object (no device needed)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `make -C {CSRC}` or __graft_entry__.build(). "
+            "qamr has no CPU fallback.")
+    L = C.CDLL(LIB_PATH)
+    for name, args in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPE.get(name, C.c_int)
+    _lib = L
+    return L
+
+
+def last_error() -> str:
+    msg = load().qr_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str = ""):
+    if rc == QR_OK:
+        return
+    msg = last_error() or what
+    if rc == QR_EVALUE:
+        raise ValueError(msg)
+    if rc == QR_EMEMORY:
+        raise MemoryError(msg)
+    raise QamrError(f"{what}: {msg}" if what else msg)
+
+
+def device_count() -> int:
+    n = i32(0)
+    load().qr_device_count(C.byref(n))
+    return int(n.value)
+
+
+def require_gpu():
+    if device_count() <= 0:
+        raise QamrError("no HIP device visible: qamr runs only on the GPU (no CPU fallback)")
+
+
+def ptr(a: np.ndarray):
+    return C.c_void_p(a.ctypes.data)
+
+
+# ------------------------------------------------------------------ profiling
+def profile_enable(on: bool = True):
+    check(load().qr_profile_enable(1 if on else 0))
+
+
+def profile_reset():
+    check(load().qr_profile_reset())
+
+
+def profile_query(name: str):
+    ms, n = f64(0), i64(0)
+    check(load().qr_profile_query(name.encode(), C.byref(ms), C.byref(n)))
+    return float(ms.value), int(n.value)

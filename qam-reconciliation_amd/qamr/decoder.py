@@ -1,0 +1,231 @@
+"""Drop-in ``Decoder`` backed by the gfx950 sum-product kernels of libqamr.so.
+
+Mirrors qamreconciliation.decoder.Decoder (decoder.pyx:92-455): same
+constructor, properties, method names, argument order, return tuples and
+exception types.  Differences (documented, stricter): input lengths are
+validated (the reference reads out of bounds, decoder.pyx:441-455), and check
+nodes of degree < 2 are rejected at construction (undefined behaviour in the
+reference, decoder.pyx:135-141).
+
+Besides the one-frame API, ``decode_batch`` (host arrays, frame-major) and
+``decode_device`` (torch tensors resident in HBM, frame-innermost layout) decode
+many independent frames per launch -- the path the benchmark measures.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, ptr
+
+
+def _as_buffer(a, dtype, name, expected):
+    """Cython typed-memoryview semantics: exact dtype, 1-D (decoder.pxd)."""
+    arr = np.asarray(a)
+    if arr.dtype == np.bool_ and dtype == np.uint8:
+        arr = arr.view(np.uint8)
+    if arr.dtype != dtype:
+        raise ValueError(f"Buffer dtype mismatch, expected '{expected}' but got '{arr.dtype}' ({name})")
+    if arr.ndim != 1:
+        raise ValueError(f"Buffer has wrong number of dimensions (expected 1, got {arr.ndim}) ({name})")
+    return np.ascontiguousarray(arr)
+
+
+def _as_inout(a, dtype, name, expected):
+    """In/out buffers must be written in place: exact dtype, 1-D, contiguous."""
+    if not isinstance(a, np.ndarray):
+        raise ValueError(f"{name} must be a numpy array (written in place)")
+    if a.dtype != dtype:
+        raise ValueError(f"Buffer dtype mismatch, expected '{expected}' but got '{a.dtype}' ({name})")
+    if a.ndim != 1 or not a.flags.c_contiguous or not a.flags.writeable:
+        raise ValueError(f"{name} must be a writeable 1-D C-contiguous array")
+    return a
+
+
+class Decoder:
+    """``Decoder(e_to_v, e_to_c)`` -- Tanner graph given as an edge list."""
+
+    def __init__(self, e_to_v, e_to_c, device: int = 0):
+        vid = _as_buffer(e_to_v, np.int64, "e_to_v", "long")
+        cid = _as_buffer(e_to_c, np.int64, "e_to_c", "long")
+        L = _lib.load()
+        h = C.c_void_p()
+        check(L.qr_code_create(ptr(vid), ptr(cid), vid.size, cid.size, int(device), C.byref(h)), "Decoder")
+        self._h = h
+        self._device = int(device)
+        v, c, e = C.c_int64(), C.c_int64(), C.c_int64()
+        dc, dv = C.c_int32(), C.c_int32()
+        check(L.qr_code_info(h, C.byref(v), C.byref(c), C.byref(e), C.byref(dc), C.byref(dv)))
+        self._V, self._C, self._E = int(v.value), int(c.value), int(e.value)
+        self.max_check_degree, self.max_var_degree = int(dc.value), int(dv.value)
+        self._ws = None  # device workspace (torch tensor) for decode_device
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _lib._lib is not None:
+            _lib._lib.qr_code_destroy(h)
+            self._h = None
+
+    # ---------------------------------------------------------- properties
+    @property
+    def cnum(self):
+        """Number of check nodes (decoder.pyx:157-160)"""
+        return self._C
+
+    @property
+    def vnum(self):
+        """Number of variable nodes (decoder.pyx:163-166)"""
+        return self._V
+
+    @property
+    def ednum(self):
+        """Number of edges (decoder.pyx:169-172)"""
+        return self._E
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def device(self):
+        return self._device
+
+    # ------------------------------------------------------ syndrome checks
+    def _check_word_flags(self, word, synd):
+        w = _as_buffer(word, np.uint8, "word", "unsigned char")
+        s = _as_buffer(synd, np.uint8, "synd", "unsigned char")
+        if w.size != self._V:
+            raise ValueError("Size of word does not match number of vnodes")
+        if s.size != self._C:
+            raise ValueError("Size of synd does not match number of cnodes")
+        flags = np.empty(self._C, np.uint8)
+        allok = C.c_uint8()
+        check(_lib.load().qr_check_word_host(self._h, ptr(w), ptr(s), ptr(flags), C.byref(allok)), "check_word")
+        return flags, int(allok.value)
+
+    def check_synd_node(self, check_node_index, word, synd):
+        """decoder.pyx:190-209: ``parity ^ 1`` of one check for a hard word."""
+        flags, _ = self._check_word_flags(word, synd)
+        return int(flags[int(check_node_index)])
+
+    def check_word(self, word, synd):
+        """decoder.pyx:220-232: 1 iff every check is satisfied by the hard word."""
+        _, allok = self._check_word_flags(word, synd)
+        return allok
+
+    def check_lappr(self, lappr, synd):
+        """decoder.pyx:260-281: 1 iff sign(lappr) (< 0 -> bit 1) satisfies synd."""
+        l = _as_buffer(lappr, np.float64, "lappr", "double")
+        s = _as_buffer(synd, np.uint8, "synd", "unsigned char")
+        if l.size != self._V:
+            raise ValueError("Size of lappr does not match number of vnodes")
+        if s.size != self._C:
+            raise ValueError("Size of synd does not match number of cnodes")
+        flags = np.empty(self._C, np.uint8)
+        allok = C.c_uint8()
+        check(_lib.load().qr_check_lappr_host(self._h, ptr(l), ptr(s), ptr(flags), C.byref(allok)), "check_lappr")
+        return int(allok.value)
+
+    # ------------------------------------------------------ node processing
+    def process_var_node(self, node_index, lappr_data, check_to_var, var_to_check, updated_lappr):
+        """decoder.pyx:301-319 (writes var_to_check and updated_lappr in place)."""
+        l = _as_buffer(lappr_data, np.float64, "lappr_data", "double")
+        c2v = _as_buffer(check_to_var, np.float64, "check_to_var", "double")
+        v2c = _as_inout(var_to_check, np.float64, "var_to_check", "double")
+        upd = _as_inout(updated_lappr, np.float64, "updated_lappr", "double")
+        if l.size < self._V or upd.size < self._V or c2v.size < self._E or v2c.size < self._E:
+            raise ValueError("message/LAPPR arrays are shorter than the graph")
+        nodes = np.array([int(node_index)], np.int64)
+        check(_lib.load().qr_process_var_nodes_host(self._h, ptr(nodes), 1, ptr(l), ptr(c2v), ptr(v2c), ptr(upd)),
+              "process_var_node")
+
+    def process_check_node(self, node_index, synd, check_to_var, var_to_check):
+        """decoder.pyx:372-388 (writes check_to_var in place); returns 0."""
+        s = _as_buffer(synd, np.uint8, "synd", "unsigned char")
+        c2v = _as_inout(check_to_var, np.float64, "check_to_var", "double")
+        v2c = _as_buffer(var_to_check, np.float64, "var_to_check", "double")
+        if s.size < self._C or c2v.size < self._E or v2c.size < self._E:
+            raise ValueError("message/syndrome arrays are shorter than the graph")
+        nodes = np.array([int(node_index)], np.int64)
+        check(_lib.load().qr_process_check_nodes_host(self._h, ptr(nodes), 1, ptr(s), ptr(c2v), ptr(v2c)),
+              "process_check_node")
+        return 0
+
+    # ---------------------------------------------------------------- decode
+    def decode(self, lappr_data, synd, max_iterations):
+        """decoder.pyx:441-455 -> (success, iterations, final_lappr)."""
+        l = _as_buffer(lappr_data, np.float64, "lappr_data", "double")
+        s = _as_buffer(synd, np.uint8, "synd", "unsigned char")
+        if l.size != self._V:
+            raise ValueError(f"lappr has {l.size} entries, the code has {self._V} variable nodes")
+        if s.size != self._C:
+            raise ValueError(f"synd has {s.size} entries, the code has {self._C} check nodes")
+        succ, its, res = self.decode_batch(l[None, :], s[None, :], max_iterations)
+        return int(succ[0]), int(its[0]), res[0]
+
+    def decode_batch(self, lappr, synd, max_iterations):
+        """Decode B independent frames from host memory.
+
+        lappr: float64 [B, V]; synd: uint8/bool [B, C].
+        Returns (success uint8[B], iterations int32[B], final float64[B, V])."""
+        l = np.ascontiguousarray(lappr)
+        s = np.asarray(synd)
+        if s.dtype == np.bool_:
+            s = s.view(np.uint8)
+        s = np.ascontiguousarray(s)
+        if l.dtype != np.float64 or s.dtype != np.uint8:
+            raise ValueError("decode_batch expects float64 LAPPRs and uint8 syndromes")
+        if l.ndim != 2 or s.ndim != 2 or l.shape[0] != s.shape[0]:
+            raise ValueError("decode_batch expects lappr [B, V] and synd [B, C]")
+        if l.shape[1] != self._V or s.shape[1] != self._C:
+            raise ValueError("decode_batch: shape does not match the code")
+        B = l.shape[0]
+        out = np.empty_like(l)
+        succ = np.empty(B, np.uint8)
+        its = np.empty(B, np.int32)
+        check(_lib.load().qr_decode_host(self._h, B, ptr(l), ptr(s), int(max_iterations), ptr(out), ptr(succ),
+                                         ptr(its)), "decode")
+        return succ, its, out
+
+    # ------------------------------------------------------- device (HBM) API
+    def workspace_bytes(self, ld: int, max_iterations: int) -> int:
+        n = C.c_size_t()
+        check(_lib.load().qr_decode_workspace_size(self._h, int(ld), int(max_iterations), C.byref(n)))
+        return int(n.value)
+
+    def decode_device(self, lappr_fi, synd_fi, B: int, max_iterations: int, final_fi=None, success=None,
+                      iters=None, stream=None):
+        """Decode B frames resident in HBM (torch tensors, frame-innermost).
+
+        lappr_fi: float64 [V, ld]; synd_fi: uint8 [C, ld]; ld % 64 == 0, B <= ld.
+        Returns (final_fi float64 [V, ld], success uint8 [B], iters int32 [B]).
+        Asynchronous on ``stream`` (default: torch's current stream)."""
+        import torch
+
+        V, ld = lappr_fi.shape
+        if V != self._V or synd_fi.shape != (self._C, ld):
+            raise ValueError("decode_device: tensor shapes do not match the code")
+        if lappr_fi.dtype != torch.float64 or synd_fi.dtype != torch.uint8:
+            raise ValueError("decode_device: expected float64 LAPPRs and uint8 syndromes")
+        if not (lappr_fi.is_contiguous() and synd_fi.is_contiguous()):
+            raise ValueError("decode_device: tensors must be contiguous")
+        dev = lappr_fi.device
+        if final_fi is None:
+            final_fi = torch.empty_like(lappr_fi)
+        if success is None:
+            success = torch.empty(B, dtype=torch.uint8, device=dev)
+        if iters is None:
+            iters = torch.empty(B, dtype=torch.int32, device=dev)
+        need = self.workspace_bytes(ld, max_iterations)
+        if self._ws is None or self._ws.numel() < need or self._ws.device != dev:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        check(_lib.load().qr_decode_batch_device(
+            self._h, int(B), int(ld), C.c_void_p(lappr_fi.data_ptr()), C.c_void_p(synd_fi.data_ptr()),
+            int(max_iterations), C.c_void_p(final_fi.data_ptr()), C.c_void_p(success.data_ptr()),
+            C.c_void_p(iters.data_ptr()), C.c_void_p(self._ws.data_ptr()), self._ws.numel(),
+            C.c_void_p(stream.cuda_stream)), "decode_device")
+        return final_fi, success, iters

@@ -1,0 +1,130 @@
+"""GPU parity tests of the soft demapper and the Bob-side producers against the
+reference's golden outputs and the oracle."""
+import numpy as np
+import pytest
+
+from conftest import assert_llr_close, golden
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+KEYS = [("b2_s30", 2), ("b2_s40", 2), ("b2_s95", 2), ("b4_s130", 4), ("b4_s145", 4), ("b4_s250", 4)]
+
+
+def _nm(bps, nv, cfg=None):
+    import qamr
+    return qamr.NoiseMapper(qamr.PAMAlphabet(bps, 2.0), nv, cfg)
+
+
+@pytest.mark.parametrize("key,bps", KEYS)
+def test_tables_and_demap_vs_reference(gpu, key, bps):
+    g = golden("demap.npz")
+    nv = float(g[f"{key}_noise_var"])
+    nm = _nm(bps, nv, g[f"{key}_cfg"])
+    # host tables: scipy-exact erf in libqamr's host code -> bit-exact
+    assert np.array_equal(nm.F_Y_thresholds, g[f"{key}_Fthr"])
+    assert np.array_equal(nm.delta_F_Y, g[f"{key}_dF"])
+    l = nm.demap_lappr_array(g[f"{key}_nhat"], g[f"{key}_x"])
+    assert_llr_close(l, g[f"{key}_lappr"])
+    nm0 = _nm(bps, nv)
+    assert_llr_close(nm0.demap_lappr_array(g[f"{key}_nhat"][:20], g[f"{key}_x"][:20]), g[f"{key}_lappr_base"])
+
+
+@pytest.mark.parametrize("key,bps", KEYS)
+def test_bob_side_vs_reference(gpu, key, bps):
+    g = golden("demap.npz")
+    nm = _nm(bps, float(g[f"{key}_noise_var"]), g[f"{key}_cfg"])
+    xh = nm.hard_decide_index(g[f"{key}_y"])
+    assert np.array_equal(xh, g[f"{key}_xhat"])
+    nh = nm.map_noise(g[f"{key}_y"], xh)
+    assert_llr_close(nh, g[f"{key}_nhat"], rtol=1e-12, atol=1e-15)
+
+
+def test_demap_device_layout_and_alpha(gpu):
+    """Batched demap writes the decoder's frame-innermost layout; alpha scales."""
+    import torch
+
+    g = golden("demap.npz")
+    key, bps = "b2_s30", 2
+    nm = _nm(bps, float(g[f"{key}_noise_var"]), g[f"{key}_cfg"])
+    n, x = g[f"{key}_nhat"], g[f"{key}_x"]
+    S = 100
+    B, ld = 3, 64
+    dev = torch.device("cuda", 0)
+    nt = torch.zeros((S, ld), dtype=torch.float64, device=dev)
+    xt = torch.zeros((S, ld), dtype=torch.int64, device=dev)
+    for f in range(B):  # frame f = the golden symbols shifted by f
+        nt[:, f] = torch.from_numpy(np.roll(n, f)[:S])
+        xt[:, f] = torch.from_numpy(np.roll(x, f)[:S])
+    out = nm.demap_device(nt, xt, B, alpha=0.75)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    ref = g[f"{key}_lappr"].reshape(-1, bps)
+    for f in range(B):
+        exp = (np.roll(ref, f, axis=0)[:S] * 0.75).reshape(-1)
+        assert_llr_close(o[:, f], exp)
+
+
+def test_demap_random_vs_oracle(gpu):
+    rng = np.random.default_rng(4)
+    for bps, nv in ((1, 0.7), (2, 0.4), (3, 1.1), (4, 0.9)):
+        M = 1 << bps
+        cfg = rng.integers(0, 2, M).astype(np.uint8)
+        nm = _nm(bps, nv, cfg)
+        onm = O.OracleNoiseMapper(bps, 2.0, nv, cfg)
+        S = 300
+        n = rng.uniform(0, 1, S)
+        n[:3] = [0.0, 1.0, 0.5]
+        x = rng.integers(0, M, S)
+        assert_llr_close(nm.demap_lappr_array(n, x), onm.demap_lappr_array(n, x))
+
+
+def test_demap_errors(gpu):
+    nm = _nm(2, 1.0)
+    with pytest.raises(ValueError):
+        nm.demap_lappr_array(np.zeros(3), np.zeros(4, np.int64))
+    with pytest.raises(ValueError):
+        nm.demap_lappr_array(np.zeros(3, np.float32), np.zeros(3, np.int64))
+    import qamr
+    with pytest.raises(ValueError):
+        qamr.NoiseMapper(qamr.PAMAlphabet(2, 2.0), 0.0)
+    with pytest.raises(ValueError):
+        qamr.NoiseMapper(qamr.PAMAlphabet(2, 2.0), 1.0, np.zeros(2, np.uint8))
+    out = nm.demap_lappr_array(np.array([0.5]), np.array([7], np.int64))  # bad symbol index -> NaN
+    assert np.isnan(out).all()
+
+
+def test_syndrome_and_counters_vs_oracle(gpu):
+    import torch
+    import qamr
+    from qamr import codes
+    from qamr.pipeline import SofteningPipeline
+
+    vid, cid = codes.regular_code(1008)
+    dec = qamr.Decoder(vid, cid)
+    orc = O.OracleCode(vid, cid)
+    pipe = SofteningPipeline(dec, 2, 3.0, batch=130, max_iterations=20)
+    gen = torch.Generator(device="cuda").manual_seed(1)
+    b, l, fin, succ, its = pipe.run_batch(gen)
+    torch.cuda.synchronize()
+    word = b.word[:, :130].cpu().numpy().T.copy()
+    synd = b.synd[:, :130].cpu().numpy().T
+    for f in range(0, 130, 13):
+        assert np.array_equal(synd[f], orc.eval_syndrome(word[f]))
+    # Bob + demap vs oracle on a few frames
+    onm = O.OracleNoiseMapper(2, 2.0, pipe.noise_var, np.array([0, 1, 0, 1], np.uint8))
+    nh = b.nhat[:, :130].cpu().numpy().T
+    xx = b.x[:, :130].cpu().numpy().T
+    lap = l[:, :130].cpu().numpy().T
+    for f in (0, 64, 129):
+        assert_llr_close(lap[f], onm.demap_lappr_array(nh[f], xx[f]))
+    # decode vs oracle, then BER/FER counters vs utils.count_errors_from_lappr
+    s2, i2, f2 = orc.decode_batch(lap, synd, 20)
+    assert np.array_equal(succ.cpu().numpy(), s2) and np.array_equal(its.cpu().numpy(), i2)
+    finv = fin[:, :130].cpu().numpy().T
+    K = pipe.K
+    errs = np.array([qamr.count_errors_from_lappr(finv[f, :K], word[f, :K]) for f in range(130)])
+    c = pipe.counters.cpu().numpy()
+    assert c[0] == errs.sum() and c[1] == (errs > 0).sum() and c[2] == s2.sum()
+    assert c[3] == i2[s2 == 1].sum() and c[4] == 130
