@@ -64,6 +64,12 @@ QR_API int qr_profile_reset(void);
  * "parity", "demap", "bob", "syndrome", "count".  Synchronises pending events. */
 QR_API int qr_profile_query(const char *name, double *total_ms, int64_t *launches);
 
+/* Kernel-geometry knobs (process-wide; performance only, results unchanged):
+ * "check_ft"/"var_ft" frames per workgroup (64/128/256), "check_per"/"var_per"
+ * nodes per thread, "nt" non-temporal edge-message stream (0/1). */
+QR_API int qr_tune_set(const char *name, int64_t value);
+QR_API int qr_tune_get(const char *name, int64_t *value);
+
 /* ------------------------------------------------------------ Tanner graph */
 /* Replaces Decoder.__cinit__ (decoder.pyx:93-146).  e_to_v / e_to_c: host int64
  * edge lists (edge e joins variable e_to_v[e] and check e_to_c[e]).  V = max+1,

@@ -22,29 +22,58 @@
 //   k_var                            post(t) = lappr + sum c2v (ascending edge)
 // plus an initial parity check of the input (decoder.pyx:400-405) and a final
 // parity check after the last sweep.
+#include <atomic>
+
+#include "fastmath.hpp"
 #include "qamr_internal.hpp"
 
 namespace qr {
 
 enum CheckMode { kFirst = 0, kNormal = 1, kParityOnly = 2 };
 
-// One lane = one (check, frame).  A block = `blockDim.x` consecutive frames
-// (all lanes of a wave share the check, so chk_* loads are scalar) walking
-// `cpb` checks of one degree class.
-template <int D, int MODE>
-__global__ void __launch_bounds__(256) k_check(const int32_t *__restrict__ checks, int64_t n_checks, int cpb,
+// Edge-message access: NT = non-temporal (streamed once per sweep; keeps the
+// re-read posteriors resident in L2/MALL instead of the message stream).
+template <bool NT>
+__device__ __forceinline__ double ld_msg(const double *p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st_msg(double *p, double v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// Block geometry shared by the check and variable sweeps: 256 threads = `ft`
+// consecutive frames (ft = 64 << lft, a multiple of the wavefront) x (256/ft)
+// node lanes; every wave therefore covers 64 frames of ONE node, which makes
+// the node index wave-uniform (readfirstlane -> scalar loads of the CSR).
+struct Geom {
+    int lft;  // log2(ft)
+    int per;  // nodes per thread
+};
+
+// One lane = one (check, frame); each thread walks `per` checks of one degree class.
+template <int D, int MODE, bool NT>
+__global__ void __launch_bounds__(256) k_check(const int32_t *__restrict__ checks, int64_t n_checks, Geom g,
                                                const int32_t *__restrict__ chk_ptr,
                                                const int32_t *__restrict__ chk_edge,
                                                const int32_t *__restrict__ chk_var, const double *__restrict__ post,
                                                double *__restrict__ c2v, const uint8_t *__restrict__ synd,
                                                const uint8_t *__restrict__ active, uint8_t *__restrict__ unsat,
-                                               int ld) {
-    const int f = blockIdx.y * blockDim.x + threadIdx.x;
+                                               int ld, const MathTables *__restrict__ gtab) {
+    __shared__ MathTables tab;
+    if (MODE != kParityOnly) stage_math_tables(&tab, gtab);
+    const int ft = 1 << g.lft;
+    const int nsub = 256 >> g.lft;
+    const int f = (blockIdx.y << g.lft) + (threadIdx.x & (ft - 1));
+    const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> g.lft);
     if (!active[f]) return;
-    const int64_t c0 = (int64_t)blockIdx.x * cpb;
-    const int64_t c1 = (c0 + cpb < n_checks) ? c0 + cpb : n_checks;
+    const int64_t c0 = (int64_t)blockIdx.x * g.per * nsub + sub;
     uint32_t bad = 0;
-    for (int64_t ci = c0; ci < c1; ++ci) {
+    for (int j = 0; j < g.per; ++j) {
+        const int64_t ci = c0 + (int64_t)j * nsub;
+        if (ci >= n_checks) break;
         const int c = checks[ci];
         const int base = chk_ptr[c];
         const uint8_t sb = synd[(size_t)c * ld + f];
@@ -54,7 +83,7 @@ __global__ void __launch_bounds__(256) k_check(const int32_t *__restrict__ check
         for (int i = 0; i < D; ++i) {
             const double p = post[(size_t)chk_var[base + i] * ld + f];
             if (MODE != kFirst) par ^= (p < 0.0) ? 1u : 0u;   // decoder.pyx:243-246
-            if (MODE == kNormal) m[i] = p - c2v[(size_t)chk_edge[base + i] * ld + f];  // :296-297
+            if (MODE == kNormal) m[i] = p - ld_msg<NT>(&c2v[(size_t)chk_edge[base + i] * ld + f]);  // :296-297
             else m[i] = p;  // first sweep: c2v == 0 and p - 0.0 == p
         }
         if (MODE != kFirst) bad |= (par == 1u) ? 1u : 0u;  // satisfied iff (parity ^ 1) != 0
@@ -63,15 +92,16 @@ __global__ void __launch_bounds__(256) k_check(const int32_t *__restrict__ check
         double F[D], Bk[D];
         F[0] = m[0];
 #pragma unroll
-        for (int i = 1; i < D - 1; ++i) F[i] = box_plus(F[i - 1], m[i]);
+        for (int i = 1; i < D - 1; ++i) F[i] = box_plus_fast(F[i - 1], m[i], tab);
         Bk[D - 1] = m[D - 1];
 #pragma unroll
-        for (int i = D - 2; i > 0; --i) Bk[i] = box_plus(Bk[i + 1], m[i]);
+        for (int i = D - 2; i > 0; --i) Bk[i] = box_plus_fast(Bk[i + 1], m[i], tab);
         const double s = sb ? -1.0 : 1.0;
-        c2v[(size_t)chk_edge[base] * ld + f] = s * Bk[1];
+        st_msg<NT>(&c2v[(size_t)chk_edge[base] * ld + f], s * Bk[1]);
 #pragma unroll
-        for (int i = 1; i < D - 1; ++i) c2v[(size_t)chk_edge[base + i] * ld + f] = s * box_plus(F[i - 1], Bk[i + 1]);
-        c2v[(size_t)chk_edge[base + D - 1] * ld + f] = s * F[D - 2];
+        for (int i = 1; i < D - 1; ++i)
+            st_msg<NT>(&c2v[(size_t)chk_edge[base + i] * ld + f], s * box_plus_fast(F[i - 1], Bk[i + 1], tab));
+        st_msg<NT>(&c2v[(size_t)chk_edge[base + D - 1] * ld + f], s * F[D - 2]);
     }
     if (MODE != kFirst && bad) unsat[f] = 1;  // benign race: every writer stores 1
 }
@@ -79,33 +109,41 @@ __global__ void __launch_bounds__(256) k_check(const int32_t *__restrict__ check
 // Runtime-degree fallback for check degrees above the templated range (2..16).
 constexpr int kMaxGenericDeg = 64;
 
-__device__ __forceinline__ void check_update_generic(int d, const double *m, double *out, double s) {
+__device__ __forceinline__ void check_update_generic(int d, const double *m, double *out, double s,
+                                                     const MathTables &tab) {
     double F[kMaxGenericDeg], Bk[kMaxGenericDeg];
     F[0] = m[0];
-    for (int i = 1; i < d - 1; ++i) F[i] = box_plus(F[i - 1], m[i]);
+    for (int i = 1; i < d - 1; ++i) F[i] = box_plus_fast(F[i - 1], m[i], tab);
     Bk[d - 1] = m[d - 1];
-    for (int i = d - 2; i > 0; --i) Bk[i] = box_plus(Bk[i + 1], m[i]);
+    for (int i = d - 2; i > 0; --i) Bk[i] = box_plus_fast(Bk[i + 1], m[i], tab);
     out[0] = s * Bk[1];
-    for (int i = 1; i < d - 1; ++i) out[i] = s * box_plus(F[i - 1], Bk[i + 1]);
+    for (int i = 1; i < d - 1; ++i) out[i] = s * box_plus_fast(F[i - 1], Bk[i + 1], tab);
     out[d - 1] = s * F[d - 2];
 }
 
 template <int MODE>
-__global__ void __launch_bounds__(256) k_check_generic(const int32_t *__restrict__ checks, int64_t n_checks, int cpb,
+__global__ void __launch_bounds__(256) k_check_generic(const int32_t *__restrict__ checks, int64_t n_checks, Geom g,
                                                        const int32_t *__restrict__ chk_ptr,
                                                        const int32_t *__restrict__ chk_edge,
                                                        const int32_t *__restrict__ chk_var,
                                                        const double *__restrict__ post, double *__restrict__ c2v,
                                                        const uint8_t *__restrict__ synd,
                                                        const uint8_t *__restrict__ active,
-                                                       uint8_t *__restrict__ unsat, int ld) {
-    const int f = blockIdx.y * blockDim.x + threadIdx.x;
+                                                       uint8_t *__restrict__ unsat, int ld,
+                                                       const MathTables *__restrict__ gtab) {
+    __shared__ MathTables tab;
+    if (MODE != kParityOnly) stage_math_tables(&tab, gtab);
+    const int ft = 1 << g.lft;
+    const int nsub = 256 >> g.lft;
+    const int f = (blockIdx.y << g.lft) + (threadIdx.x & (ft - 1));
+    const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> g.lft);
     if (!active[f]) return;
-    const int64_t c0 = (int64_t)blockIdx.x * cpb;
-    const int64_t c1 = (c0 + cpb < n_checks) ? c0 + cpb : n_checks;
+    const int64_t c0 = (int64_t)blockIdx.x * g.per * nsub + sub;
     uint32_t bad = 0;
     double m[kMaxGenericDeg], out[kMaxGenericDeg];
-    for (int64_t ci = c0; ci < c1; ++ci) {
+    for (int j = 0; j < g.per; ++j) {
+        const int64_t ci = c0 + (int64_t)j * nsub;
+        if (ci >= n_checks) break;
         const int c = checks[ci];
         const int base = chk_ptr[c];
         const int d = chk_ptr[c + 1] - base;
@@ -118,7 +156,7 @@ __global__ void __launch_bounds__(256) k_check_generic(const int32_t *__restrict
         }
         if (MODE != kFirst) bad |= (par == 1u) ? 1u : 0u;
         if (MODE == kParityOnly) continue;
-        check_update_generic(d, m, out, sb ? -1.0 : 1.0);
+        check_update_generic(d, m, out, sb ? -1.0 : 1.0, tab);
         for (int i = 0; i < d; ++i) c2v[(size_t)chk_edge[base + i] * ld + f] = out[i];
     }
     if (MODE != kFirst && bad) unsat[f] = 1;
@@ -128,23 +166,27 @@ __global__ void __launch_bounds__(256) k_check_generic(const int32_t *__restrict
 // INIT: the first sweep with c2v == 0 (decoder.pyx:408,420-421): lappr + 0.0 for
 // frames still decoding; frames already successful at iteration 0 get a plain
 // copy of their input (decoder.pyx:404).
-template <bool INIT>
-__global__ void __launch_bounds__(256) k_var(int64_t V, int vpb, const int32_t *__restrict__ var_ptr,
+template <bool INIT, bool NT>
+__global__ void __launch_bounds__(256) k_var(int64_t V, Geom g, const int32_t *__restrict__ var_ptr,
                                              const int32_t *__restrict__ var_edge, const double *__restrict__ lappr,
                                              const double *__restrict__ c2v, double *__restrict__ post,
                                              const uint8_t *__restrict__ active, int ld) {
-    const int f = blockIdx.y * blockDim.x + threadIdx.x;
+    const int ft = 1 << g.lft;
+    const int nsub = 256 >> g.lft;
+    const int f = (blockIdx.y << g.lft) + (threadIdx.x & (ft - 1));
+    const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> g.lft);
     const bool act = active[f] != 0;
     if (!INIT && !act) return;
-    const int64_t v0 = (int64_t)blockIdx.x * vpb;
-    const int64_t v1 = (v0 + vpb < V) ? v0 + vpb : V;
-    for (int64_t v = v0; v < v1; ++v) {
+    const int64_t v0 = (int64_t)blockIdx.x * g.per * nsub + sub;
+    for (int j = 0; j < g.per; ++j) {
+        const int64_t v = v0 + (int64_t)j * nsub;
+        if (v >= V) break;
         const int b = var_ptr[v], e = var_ptr[v + 1];
-        double p = lappr[(size_t)v * ld + f];
+        double p = ld_msg<NT>(&lappr[(size_t)v * ld + f]);
         if (INIT) {
             if (act && e > b) p = p + 0.0;
         } else {
-            for (int k = b; k < e; ++k) p += c2v[(size_t)var_edge[k] * ld + f];
+            for (int k = b; k < e; ++k) p += ld_msg<NT>(&c2v[(size_t)var_edge[k] * ld + f]);
         }
         post[(size_t)v * ld + f] = p;
     }
@@ -202,31 +244,43 @@ static DecodeWs carve(const qr_code *code, int ld, void *base) {
     return w;
 }
 
-constexpr int kChecksPerBlock = 4;
-constexpr int kVarsPerBlock = 4;
+// Runtime tuning knobs (qr_tune_set); defaults picked by scripts/tune.py on MI355X.
+struct Tuning {
+    std::atomic<int> check_ft{256}, check_per{4}, var_ft{256}, var_per{4}, nt{1};
+};
+static Tuning g_tune;
 
-template <int MODE>
+static Geom make_geom(int ld, int ft_req, int per) {
+    int ft = 256;
+    while (ft > 64 && (ft > ft_req || ld % ft)) ft >>= 1;
+    int lft = 6;
+    while ((1 << lft) < ft) ++lft;
+    return Geom{lft, per < 1 ? 1 : per};
+}
+
+template <int MODE, bool NT>
 static int launch_check_class(const qr_code *code, const DegreeClass &cls, int ld, const double *post, double *c2v,
                               const uint8_t *synd, const uint8_t *active, uint8_t *unsat, hipStream_t s) {
-    const int ft = frame_tile(ld);
-    dim3 grid((unsigned)((cls.n + kChecksPerBlock - 1) / kChecksPerBlock), (unsigned)(ld / ft));
+    const Geom g = make_geom(ld, g_tune.check_ft.load(), g_tune.check_per.load());
+    const int64_t per_block = (int64_t)g.per * (256 >> g.lft);
+    dim3 grid((unsigned)((cls.n + per_block - 1) / per_block), (unsigned)(ld >> g.lft));
     ProfScope ps(profiling_on() ? std::string(MODE == kParityOnly ? "parity_d" : MODE == kFirst ? "check1_d" : "check_d") +
                                       std::to_string(cls.degree)
                                 : std::string(),
                  s);
-#define QR_CASE(DD)                                                                                             \
-    case DD:                                                                                                    \
-        k_check<DD, MODE><<<grid, ft, 0, s>>>(cls.d_checks, cls.n, kChecksPerBlock, code->d_chk_ptr,            \
-                                              code->d_chk_edge, code->d_chk_var, post, c2v, synd, active, unsat, \
-                                              ld);                                                              \
+#define QR_CASE(DD)                                                                                          \
+    case DD:                                                                                                 \
+        k_check<DD, MODE, NT><<<grid, 256, 0, s>>>(cls.d_checks, cls.n, g, code->d_chk_ptr, code->d_chk_edge, \
+                                                   code->d_chk_var, post, c2v, synd, active, unsat, ld,        \
+                                                   code->d_mtab);                                             \
         break;
     switch (cls.degree) {
         QR_CASE(2) QR_CASE(3) QR_CASE(4) QR_CASE(5) QR_CASE(6) QR_CASE(7) QR_CASE(8) QR_CASE(9) QR_CASE(10)
         QR_CASE(11) QR_CASE(12) QR_CASE(13) QR_CASE(14) QR_CASE(15) QR_CASE(16)
         default:
-            k_check_generic<MODE><<<grid, ft, 0, s>>>(cls.d_checks, cls.n, kChecksPerBlock, code->d_chk_ptr,
-                                                      code->d_chk_edge, code->d_chk_var, post, c2v, synd, active,
-                                                      unsat, ld);
+            k_check_generic<MODE><<<grid, 256, 0, s>>>(cls.d_checks, cls.n, g, code->d_chk_ptr, code->d_chk_edge,
+                                                       code->d_chk_var, post, c2v, synd, active, unsat, ld,
+                                                       code->d_mtab);
     }
 #undef QR_CASE
     QR_LAUNCH_CHECK();
@@ -237,8 +291,10 @@ template <int MODE>
 static int launch_check_all(const qr_code *code, int ld, const double *post, double *c2v, const uint8_t *synd,
                             const uint8_t *active, uint8_t *unsat, hipStream_t s) {
     ProfScope ps(MODE == kParityOnly ? "parity" : MODE == kFirst ? "check1" : "check", s);
+    const bool nt = g_tune.nt.load() != 0;
     for (const auto &cls : code->classes) {
-        int rc = launch_check_class<MODE>(code, cls, ld, post, c2v, synd, active, unsat, s);
+        int rc = nt ? launch_check_class<MODE, true>(code, cls, ld, post, c2v, synd, active, unsat, s)
+                    : launch_check_class<MODE, false>(code, cls, ld, post, c2v, synd, active, unsat, s);
         if (rc) return rc;
     }
     return QR_OK;
@@ -248,10 +304,15 @@ template <bool INIT>
 static int launch_var(const qr_code *code, int ld, const double *lappr, const double *c2v, double *post,
                       const uint8_t *active, hipStream_t s) {
     ProfScope ps(INIT ? "var_init" : "var", s);
-    const int ft = frame_tile(ld);
-    dim3 grid((unsigned)((code->V + kVarsPerBlock - 1) / kVarsPerBlock), (unsigned)(ld / ft));
-    k_var<INIT><<<grid, ft, 0, s>>>(code->V, kVarsPerBlock, code->d_var_ptr, code->d_var_edge, lappr, c2v, post,
-                                    active, ld);
+    const Geom g = make_geom(ld, g_tune.var_ft.load(), g_tune.var_per.load());
+    const int64_t per_block = (int64_t)g.per * (256 >> g.lft);
+    dim3 grid((unsigned)((code->V + per_block - 1) / per_block), (unsigned)(ld >> g.lft));
+    if (g_tune.nt.load())
+        k_var<INIT, true><<<grid, 256, 0, s>>>(code->V, g, code->d_var_ptr, code->d_var_edge, lappr, c2v, post,
+                                               active, ld);
+    else
+        k_var<INIT, false><<<grid, 256, 0, s>>>(code->V, g, code->d_var_ptr, code->d_var_edge, lappr, c2v, post,
+                                                active, ld);
     QR_LAUNCH_CHECK();
     return QR_OK;
 }
@@ -342,14 +403,16 @@ __global__ void k_var_nodes(const int64_t *nodes, int64_t n, const int32_t *var_
 }
 
 __global__ void k_check_nodes(const int64_t *nodes, int64_t n, const int32_t *chk_ptr, const int32_t *chk_edge,
-                              const uint8_t *synd, double *c2v, const double *v2c) {
+                              const uint8_t *synd, double *c2v, const double *v2c, const MathTables *gtab) {
+    __shared__ MathTables tab;
+    stage_math_tables(&tab, gtab);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int64_t c = nodes[i];
     const int base = chk_ptr[c], d = chk_ptr[c + 1] - base;
     double m[kMaxGenericDeg], out[kMaxGenericDeg];
     for (int k = 0; k < d; ++k) m[k] = v2c[chk_edge[base + k]];
-    check_update_generic(d, m, out, synd[c] ? -1.0 : 1.0);
+    check_update_generic(d, m, out, synd[c] ? -1.0 : 1.0, tab);
     for (int k = 0; k < d; ++k) c2v[chk_edge[base + k]] = out[k];
 }
 
@@ -367,6 +430,7 @@ static int free_code(qr_code *c) {
     (void)hipFree(c->d_chk_var);
     (void)hipFree(c->d_var_ptr);
     (void)hipFree(c->d_var_edge);
+    (void)hipFree(c->d_mtab);
     delete c;
     return QR_OK;
 }
@@ -449,6 +513,14 @@ int qr_code_create(const int64_t *e_to_v, const int64_t *e_to_c, int64_t nv, int
         free_code(code);
         return rc;
     }
+    {
+        std::vector<MathTables> mt(1);
+        build_math_tables(&mt[0]);
+        if ((rc = upload(&code->d_mtab, mt))) {
+            free_code(code);
+            return rc;
+        }
+    }
     for (int d = 0; d < (int)by_deg.size(); ++d) {
         if (by_deg[d].empty()) continue;
         DegreeClass cls{d, (int64_t)by_deg[d].size(), nullptr};
@@ -463,6 +535,27 @@ int qr_code_create(const int64_t *e_to_v, const int64_t *e_to_c, int64_t nv, int
 }
 
 int qr_code_destroy(qr_code *code) { return free_code(code); }
+
+int qr_tune_set(const char *name, int64_t value) {
+    const std::string n = name ? name : "";
+    std::atomic<int> *k = n == "check_ft" ? &g_tune.check_ft : n == "check_per" ? &g_tune.check_per
+                        : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
+                        : n == "nt"       ? &g_tune.nt       : nullptr;
+    if (!k) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
+    if (value < 0 || value > 4096) return set_error(QR_EVALUE, "tuning value out of range");
+    k->store((int)value);
+    return QR_OK;
+}
+
+int qr_tune_get(const char *name, int64_t *value) {
+    const std::string n = name ? name : "";
+    const std::atomic<int> *k = n == "check_ft" ? &g_tune.check_ft : n == "check_per" ? &g_tune.check_per
+                              : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
+                              : n == "nt"       ? &g_tune.nt       : nullptr;
+    if (!k || !value) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
+    *value = k->load();
+    return QR_OK;
+}
 
 int qr_code_info(const qr_code *code, int64_t *vnum, int64_t *cnum, int64_t *ednum, int32_t *max_dc,
                  int32_t *max_dv) {
@@ -627,7 +720,7 @@ int qr_process_check_nodes_host(const qr_code *code, const int64_t *nodes, int64
     QR_HIP(hipMemcpy(d_c2v, c2v, E * 8, hipMemcpyHostToDevice));
     QR_HIP(hipMemcpy(d_v2c, v2c, E * 8, hipMemcpyHostToDevice));
     k_check_nodes<<<(unsigned)((n + 255) / 256), 256>>>(d_nodes, n, code->d_chk_ptr, code->d_chk_edge, d_synd, d_c2v,
-                                                        d_v2c);
+                                                        d_v2c, code->d_mtab);
     QR_LAUNCH_CHECK();
     QR_HIP(hipMemcpy(c2v, d_c2v, E * 8, hipMemcpyDeviceToHost));
     return QR_OK;

@@ -9,6 +9,7 @@
 
 #include "qamr.h"
 #include "qamr_math.hpp"
+#include "fastmath.hpp"
 
 namespace qr {
 
@@ -86,6 +87,7 @@ struct qr_code {
     int32_t *d_chk_ptr = nullptr, *d_chk_edge = nullptr, *d_chk_var = nullptr;
     int32_t *d_var_ptr = nullptr, *d_var_edge = nullptr;
     std::vector<DegreeClass> classes;
+    qr::MathTables *d_mtab = nullptr;  // box-plus exp/log tables (fastmath.hpp)
     mutable qr::Scratch scratch;
 };
 

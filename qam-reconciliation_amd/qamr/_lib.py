@@ -32,6 +32,8 @@ SIGNATURES = {
     "qr_profile_enable": [i32],
     "qr_profile_reset": [],
     "qr_profile_query": [C.c_char_p, P(f64), P(i64)],
+    "qr_tune_set": [C.c_char_p, i64],
+    "qr_tune_get": [C.c_char_p, P(i64)],
     "qr_code_create": [vp, vp, i64, i64, i32, P(vp)],
     "qr_code_destroy": [vp],
     "qr_code_info": [vp, P(i64), P(i64), P(i64), P(i32), P(i32)],
@@ -79,6 +81,14 @@ def load():
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `make -C {CSRC}` or __graft_entry__.build(). "
             "qamr has no CPU fallback.")
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7.  If
+    # libqamr were loaded first it would pull /opt/rocm's copy (same soname)
+    # and torch would then load a second runtime that sees no GPU.  Importing
+    # torch first makes libqamr bind to the runtime torch already loaded.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     L = C.CDLL(LIB_PATH)
     for name, args in SIGNATURES.items():
         fn = getattr(L, name)
@@ -117,6 +127,17 @@ def require_gpu():
 
 def ptr(a: np.ndarray):
     return C.c_void_p(a.ctypes.data)
+
+
+# ------------------------------------------------------------------ tuning
+def tune_set(name: str, value: int):
+    check(load().qr_tune_set(name.encode(), int(value)))
+
+
+def tune_get(name: str) -> int:
+    v = i64(0)
+    check(load().qr_tune_get(name.encode(), C.byref(v)))
+    return int(v.value)
 
 
 # ------------------------------------------------------------------ profiling

@@ -96,6 +96,7 @@ class NoiseMapper:
                     t += p[k] * fw[k, i]
                 back[i, j] = p[j] * fw[j, i] / t
         bare = np.empty((M, self.bit_per_symbol))
+        old = np.seterr(divide="ignore")
         for j in range(M):
             for k in range(self.bit_per_symbol):
                 N = D = 0.0
@@ -105,7 +106,9 @@ class NoiseMapper:
                         D += fw[j, i]
                     else:
                         N += fw[j, i]
-                bare[j, k] = 1e300 if D == 0 else math.log(N / D)
+                # C log semantics (log(0) = -inf) rather than math.log's ValueError
+                bare[j, k] = 1e300 if D == 0 else float(np.log(np.float64(N) / np.float64(D)))
+        np.seterr(**old)
         ierf = np.empty((M, M))
         for j in range(M):
             ierf[0, j] = -1

@@ -14,7 +14,8 @@ run() {  # run <name> <seconds> <cmd...>; continue on plain test failures (rc 1)
   return 0
 }
 STEPS=${STEPS:-tests,smoke,bench}
-[[ $STEPS == *tests* ]] && run pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider
+[[ $STEPS == *tests* ]] && run pytest_gpu 900 python -m pytest tests -m gpu -q ${PYTEST_ARGS:--x} -p no:cacheprovider
 [[ $STEPS == *smoke* ]] && run smoke 300 python __graft_entry__.py smoke
+[[ $STEPS == *tune* ]] && run tune 900 python scripts/tune.py ${TUNE_ARGS:-}
 [[ $STEPS == *bench* ]] && run bench 900 python bench.py ${BENCH_ARGS:-}
 exit 0
