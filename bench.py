@@ -68,6 +68,12 @@ def setup_dist(args):
     return world, rank, local
 
 
+def var_sweep_bytes(V, E, B):
+    """Algorithmic bytes of one variable sweep over B frames: c2v read (8 B per
+    edge), lappr read and post write (8 B per variable each) -- SURVEY.md 8(d)."""
+    return (8 * E + 16 * V) * B
+
+
 def check_class_bytes(vid, cid, degree, B):
     """Algorithmic bytes of one launch of the degree-`degree` check kernel over B
     frames: c2v read + write (16 B per edge), the unique posteriors it gathers
@@ -200,28 +206,44 @@ def main():
     roof = None
     kstats = {}
     if not args.no_roofline:
-        ms7, n7 = qamr.profile_query("check_d7")
-        for k in ("check", "check_d7", "check_d6", "check1", "var", "var_init", "parity", "status", "demap"):
+        for k in ("check", "check_d7", "check_d6", "check1", "fused_d7", "var", "var_init", "parity", "status",
+                  "demap"):
             ms, n = qamr.profile_query(k)
             if n:
                 kstats[k] = {"avg_us": 1e3 * ms / n, "launches": n, "total_ms": ms}
-        if n7:
-            bytes7, shape7 = check_class_bytes(vid, cid, 7, batch.B)
-            avg_s = ms7 / n7 / 1e3
-            ach = bytes7 / avg_s / 1e9
+        V_, E_ = dec.vnum, dec.ednum
+        if "fused_d7" in kstats:
+            # split schedule: one launch = check sweep of one frame half + variable sweep of the other
+            half = batch.ld // 2
+            fr_c = min(batch.B, half)           # real frames in the checked half (first half)
+            fr_v = batch.B - fr_c if batch.B > half else 0
+            # both orientations alternate; price the average launch over both halves
+            bc0, _ = check_class_bytes(vid, cid, 7, fr_c)
+            bc1, _ = check_class_bytes(vid, cid, 7, max(batch.B - fr_c, 0))
+            bytes_launch = (bc0 + bc1) / 2 + (var_sweep_bytes(V_, E_, fr_c) + var_sweep_bytes(V_, E_, fr_v)) / 2
+            kname, kkey = "k_fused<7,Normal> (check sweep of one frame half + variable sweep of the other)", "fused_d7"
+        elif "check_d7" in kstats:
+            bytes_launch, _ = check_class_bytes(vid, cid, 7, batch.B)
+            kname, kkey = "k_check<7,Normal> (degree-7 check-node sweep)", "check_d7"
+        else:
+            kkey = None
+        if kkey:
+            avg_s = kstats[kkey]["avg_us"] / 1e6
+            ach = bytes_launch / avg_s / 1e9
             traffic = None
             pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
             if os.path.exists(pmc):
                 try:
                     t = json.load(open(pmc))
-                    if t.get("workload") == args.workload and int(t.get("batch", -1)) == batch.B:
-                        traffic = t.get("check_d7_bytes_per_launch")
+                    if t.get("workload") == args.workload and int(t.get("batch", -1)) == batch.B \
+                            and t.get("kernel_key") == kkey:
+                        traffic = t.get("hbm_bytes_per_launch")
                 except Exception:
                     traffic = None
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": "k_check<7,Normal> (degree-7 check-node sweep)",
-                    "bytes_per_launch": bytes7, "avg_launch_us": round(avg_s * 1e6, 1), "launches": n7}
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
+                    "bytes_per_launch": int(bytes_launch), "avg_launch_us": round(avg_s * 1e6, 1),
+                    "launches": kstats[kkey]["launches"]}
     # whole-decode algorithmic bandwidth (SURVEY.md 8(d) B_frame at the iterations actually run)
     it_mean = float(its.float().mean().item())
     V, C, E = dec.vnum, dec.cnum, dec.ednum

@@ -66,7 +66,10 @@ QR_API int qr_profile_query(const char *name, double *total_ms, int64_t *launche
 
 /* Kernel-geometry knobs (process-wide; performance only, results unchanged):
  * "check_ft"/"var_ft" frames per workgroup (64/128/256), "check_per"/"var_per"
- * nodes per thread, "nt" non-temporal edge-message stream (0/1). */
+ * nodes per thread, "nt" non-temporal edge-message stream (0/1), "split"
+ * (1 = all frames in lock-step, 2 = two frame halves software-pipelined half an
+ * iteration apart so each launch overlaps one half's check sweep with the
+ * other half's variable sweep). */
 QR_API int qr_tune_set(const char *name, int64_t value);
 QR_API int qr_tune_get(const char *name, int64_t *value);
 

@@ -45,7 +45,7 @@ __device__ __forceinline__ void st_msg(double *p, double v) {
 }
 
 // Block geometry shared by the check and variable sweeps: 256 threads = `ft`
-// consecutive frames (ft = 64 << lft, a multiple of the wavefront) x (256/ft)
+// consecutive frames (ft = 64 << k, a multiple of the wavefront) x (256/ft)
 // node lanes; every wave therefore covers 64 frames of ONE node, which makes
 // the node index wave-uniform (readfirstlane -> scalar loads of the CSR).
 struct Geom {
@@ -53,42 +53,64 @@ struct Geom {
     int per;  // nodes per thread
 };
 
+// One check sweep over the frame columns [f_off, f_off + ny*ft) of one degree class.
+struct CheckArgs {
+    const int32_t *checks;  // the class's check ids
+    int64_t n_checks;
+    const int32_t *chk_ptr, *chk_edge, *chk_var;
+    const double *post;
+    double *c2v;
+    const uint8_t *synd;
+    const uint8_t *active;
+    uint8_t *unsat;
+    int ld, f_off;
+    Geom g;
+    unsigned nbx;  // blocks along the check axis
+    const MathTables *gtab;
+};
+
+// One variable sweep over the frame columns [f_off, f_off + ny*ft).
+struct VarArgs {
+    int64_t V;
+    const int32_t *var_ptr, *var_edge;
+    const double *lappr, *c2v;
+    double *post;
+    const uint8_t *active;
+    int ld, f_off;
+    Geom g;
+    unsigned nbx;
+};
+
 // One lane = one (check, frame); each thread walks `per` checks of one degree class.
+// decoder.pyx:322-369 (F/B recursion) with the parity test of decoder.pyx:235-257
+// fused on the posteriors it gathers anyway.
 template <int D, int MODE, bool NT>
-__global__ void __launch_bounds__(256) k_check(const int32_t *__restrict__ checks, int64_t n_checks, Geom g,
-                                               const int32_t *__restrict__ chk_ptr,
-                                               const int32_t *__restrict__ chk_edge,
-                                               const int32_t *__restrict__ chk_var, const double *__restrict__ post,
-                                               double *__restrict__ c2v, const uint8_t *__restrict__ synd,
-                                               const uint8_t *__restrict__ active, uint8_t *__restrict__ unsat,
-                                               int ld, const MathTables *__restrict__ gtab) {
-    __shared__ MathTables tab;
-    if (MODE != kParityOnly) stage_math_tables(&tab, gtab);
-    const int ft = 1 << g.lft;
-    const int nsub = 256 >> g.lft;
-    const int f = (blockIdx.y << g.lft) + (threadIdx.x & (ft - 1));
-    const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> g.lft);
-    if (!active[f]) return;
-    const int64_t c0 = (int64_t)blockIdx.x * g.per * nsub + sub;
+__device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, unsigned by, const MathTables &tab) {
+    const int ft = 1 << a.g.lft;
+    const int nsub = 256 >> a.g.lft;
+    const int ld = a.ld;
+    const int f = a.f_off + (int)(by << a.g.lft) + (threadIdx.x & (ft - 1));
+    const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> a.g.lft);
+    if (!a.active[f]) return;
+    const int64_t c0 = (int64_t)bx * a.g.per * nsub + sub;
     uint32_t bad = 0;
-    for (int j = 0; j < g.per; ++j) {
+    for (int j = 0; j < a.g.per; ++j) {
         const int64_t ci = c0 + (int64_t)j * nsub;
-        if (ci >= n_checks) break;
-        const int c = checks[ci];
-        const int base = chk_ptr[c];
-        const uint8_t sb = synd[(size_t)c * ld + f];
+        if (ci >= a.n_checks) break;
+        const int c = a.checks[ci];
+        const int base = a.chk_ptr[c];
+        const uint8_t sb = a.synd[(size_t)c * ld + f];
         uint32_t par = sb;
         double m[D];
 #pragma unroll
         for (int i = 0; i < D; ++i) {
-            const double p = post[(size_t)chk_var[base + i] * ld + f];
+            const double p = a.post[(size_t)a.chk_var[base + i] * ld + f];
             if (MODE != kFirst) par ^= (p < 0.0) ? 1u : 0u;   // decoder.pyx:243-246
-            if (MODE == kNormal) m[i] = p - ld_msg<NT>(&c2v[(size_t)chk_edge[base + i] * ld + f]);  // :296-297
+            if (MODE == kNormal) m[i] = p - ld_msg<NT>(&a.c2v[(size_t)a.chk_edge[base + i] * ld + f]);  // :296-297
             else m[i] = p;  // first sweep: c2v == 0 and p - 0.0 == p
         }
         if (MODE != kFirst) bad |= (par == 1u) ? 1u : 0u;  // satisfied iff (parity ^ 1) != 0
         if (MODE == kParityOnly) continue;
-        // decoder.pyx:341-367
         double F[D], Bk[D];
         F[0] = m[0];
 #pragma unroll
@@ -97,13 +119,74 @@ __global__ void __launch_bounds__(256) k_check(const int32_t *__restrict__ check
 #pragma unroll
         for (int i = D - 2; i > 0; --i) Bk[i] = box_plus_fast(Bk[i + 1], m[i], tab);
         const double s = sb ? -1.0 : 1.0;
-        st_msg<NT>(&c2v[(size_t)chk_edge[base] * ld + f], s * Bk[1]);
+        st_msg<NT>(&a.c2v[(size_t)a.chk_edge[base] * ld + f], s * Bk[1]);
 #pragma unroll
         for (int i = 1; i < D - 1; ++i)
-            st_msg<NT>(&c2v[(size_t)chk_edge[base + i] * ld + f], s * box_plus_fast(F[i - 1], Bk[i + 1], tab));
-        st_msg<NT>(&c2v[(size_t)chk_edge[base + D - 1] * ld + f], s * F[D - 2]);
+            st_msg<NT>(&a.c2v[(size_t)a.chk_edge[base + i] * ld + f], s * box_plus_fast(F[i - 1], Bk[i + 1], tab));
+        st_msg<NT>(&a.c2v[(size_t)a.chk_edge[base + D - 1] * ld + f], s * F[D - 2]);
     }
-    if (MODE != kFirst && bad) unsat[f] = 1;  // benign race: every writer stores 1
+    if (MODE != kFirst && bad) a.unsat[f] = 1;  // benign race: every writer stores 1
+}
+
+// decoder.pyx:285-298: post[v] = lappr[v] + c2v[e_0] + c2v[e_1] + ... (ascending e).
+// INIT: the first sweep with c2v == 0 (decoder.pyx:408,420-421): lappr + 0.0 for
+// frames still decoding; frames already successful at iteration 0 get a plain
+// copy of their input (decoder.pyx:404).
+template <bool INIT, bool NT>
+__device__ __forceinline__ void var_block(const VarArgs &a, unsigned bx, unsigned by) {
+    const int ft = 1 << a.g.lft;
+    const int nsub = 256 >> a.g.lft;
+    const int ld = a.ld;
+    const int f = a.f_off + (int)(by << a.g.lft) + (threadIdx.x & (ft - 1));
+    const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> a.g.lft);
+    const bool act = a.active[f] != 0;
+    if (!INIT && !act) return;
+    const int64_t v0 = (int64_t)bx * a.g.per * nsub + sub;
+    for (int j = 0; j < a.g.per; ++j) {
+        const int64_t v = v0 + (int64_t)j * nsub;
+        if (v >= a.V) break;
+        const int b = a.var_ptr[v], e = a.var_ptr[v + 1];
+        double p = ld_msg<NT>(&a.lappr[(size_t)v * ld + f]);
+        if (INIT) {
+            if (act && e > b) p = p + 0.0;
+        } else {
+            for (int k = b; k < e; ++k) p += ld_msg<NT>(&a.c2v[(size_t)a.var_edge[k] * ld + f]);
+        }
+        a.post[(size_t)v * ld + f] = p;
+    }
+}
+
+template <int D, int MODE, bool NT>
+__global__ void __launch_bounds__(256) k_check(CheckArgs a) {
+    __shared__ MathTables tab;
+    if (MODE != kParityOnly) stage_math_tables(&tab, a.gtab);
+    check_block<D, MODE, NT>(a, blockIdx.x, blockIdx.y, tab);
+}
+
+template <bool INIT, bool NT>
+__global__ void __launch_bounds__(256) k_var(VarArgs a) {
+    var_block<INIT, NT>(a, blockIdx.x, blockIdx.y);
+}
+
+// One launch = the check sweep of one frame half and the variable sweep of the
+// other (they never touch the same frame columns).  The check sweep is fp64-VALU
+// bound and the variable sweep HBM bound: interleaving their workgroups (evenly
+// spread over the 1-D grid, in proportion to their counts) lets the dispatcher
+// co-schedule them on every CU, so the message stream of one hides under the
+// transcendental arithmetic of the other.
+template <int D, int MODE, bool NT>
+__global__ void __launch_bounds__(256) k_fused(CheckArgs ca, VarArgs va, unsigned nb_check, unsigned nb_total) {
+    __shared__ MathTables tab;
+    const unsigned b = blockIdx.x;
+    const unsigned c0 = (unsigned)(((uint64_t)b * nb_check) / nb_total);
+    const unsigned c1 = (unsigned)(((uint64_t)(b + 1) * nb_check) / nb_total);
+    if (c1 > c0) {  // block-uniform branch
+        stage_math_tables(&tab, ca.gtab);
+        check_block<D, MODE, NT>(ca, c0 % ca.nbx, c0 / ca.nbx, tab);
+    } else {
+        const unsigned vi = b - c0;
+        var_block<false, NT>(va, vi % va.nbx, vi / va.nbx);
+    }
 }
 
 // Runtime-degree fallback for check degrees above the templated range (2..16).
@@ -122,74 +205,37 @@ __device__ __forceinline__ void check_update_generic(int d, const double *m, dou
 }
 
 template <int MODE>
-__global__ void __launch_bounds__(256) k_check_generic(const int32_t *__restrict__ checks, int64_t n_checks, Geom g,
-                                                       const int32_t *__restrict__ chk_ptr,
-                                                       const int32_t *__restrict__ chk_edge,
-                                                       const int32_t *__restrict__ chk_var,
-                                                       const double *__restrict__ post, double *__restrict__ c2v,
-                                                       const uint8_t *__restrict__ synd,
-                                                       const uint8_t *__restrict__ active,
-                                                       uint8_t *__restrict__ unsat, int ld,
-                                                       const MathTables *__restrict__ gtab) {
+__global__ void __launch_bounds__(256) k_check_generic(CheckArgs a) {
     __shared__ MathTables tab;
-    if (MODE != kParityOnly) stage_math_tables(&tab, gtab);
-    const int ft = 1 << g.lft;
-    const int nsub = 256 >> g.lft;
-    const int f = (blockIdx.y << g.lft) + (threadIdx.x & (ft - 1));
-    const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> g.lft);
-    if (!active[f]) return;
-    const int64_t c0 = (int64_t)blockIdx.x * g.per * nsub + sub;
+    if (MODE != kParityOnly) stage_math_tables(&tab, a.gtab);
+    const int ft = 1 << a.g.lft;
+    const int nsub = 256 >> a.g.lft;
+    const int ld = a.ld;
+    const int f = a.f_off + (int)(blockIdx.y << a.g.lft) + (threadIdx.x & (ft - 1));
+    const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> a.g.lft);
+    if (!a.active[f]) return;
+    const int64_t c0 = (int64_t)blockIdx.x * a.g.per * nsub + sub;
     uint32_t bad = 0;
     double m[kMaxGenericDeg], out[kMaxGenericDeg];
-    for (int j = 0; j < g.per; ++j) {
+    for (int j = 0; j < a.g.per; ++j) {
         const int64_t ci = c0 + (int64_t)j * nsub;
-        if (ci >= n_checks) break;
-        const int c = checks[ci];
-        const int base = chk_ptr[c];
-        const int d = chk_ptr[c + 1] - base;
-        const uint8_t sb = synd[(size_t)c * ld + f];
+        if (ci >= a.n_checks) break;
+        const int c = a.checks[ci];
+        const int base = a.chk_ptr[c];
+        const int d = a.chk_ptr[c + 1] - base;
+        const uint8_t sb = a.synd[(size_t)c * ld + f];
         uint32_t par = sb;
         for (int i = 0; i < d; ++i) {
-            const double p = post[(size_t)chk_var[base + i] * ld + f];
+            const double p = a.post[(size_t)a.chk_var[base + i] * ld + f];
             if (MODE != kFirst) par ^= (p < 0.0) ? 1u : 0u;
-            m[i] = (MODE == kNormal) ? p - c2v[(size_t)chk_edge[base + i] * ld + f] : p;
+            m[i] = (MODE == kNormal) ? p - a.c2v[(size_t)a.chk_edge[base + i] * ld + f] : p;
         }
         if (MODE != kFirst) bad |= (par == 1u) ? 1u : 0u;
         if (MODE == kParityOnly) continue;
         check_update_generic(d, m, out, sb ? -1.0 : 1.0, tab);
-        for (int i = 0; i < d; ++i) c2v[(size_t)chk_edge[base + i] * ld + f] = out[i];
+        for (int i = 0; i < d; ++i) a.c2v[(size_t)a.chk_edge[base + i] * ld + f] = out[i];
     }
-    if (MODE != kFirst && bad) unsat[f] = 1;
-}
-
-// decoder.pyx:285-298: post[v] = lappr[v] + c2v[e_0] + c2v[e_1] + ... (ascending e).
-// INIT: the first sweep with c2v == 0 (decoder.pyx:408,420-421): lappr + 0.0 for
-// frames still decoding; frames already successful at iteration 0 get a plain
-// copy of their input (decoder.pyx:404).
-template <bool INIT, bool NT>
-__global__ void __launch_bounds__(256) k_var(int64_t V, Geom g, const int32_t *__restrict__ var_ptr,
-                                             const int32_t *__restrict__ var_edge, const double *__restrict__ lappr,
-                                             const double *__restrict__ c2v, double *__restrict__ post,
-                                             const uint8_t *__restrict__ active, int ld) {
-    const int ft = 1 << g.lft;
-    const int nsub = 256 >> g.lft;
-    const int f = (blockIdx.y << g.lft) + (threadIdx.x & (ft - 1));
-    const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> g.lft);
-    const bool act = active[f] != 0;
-    if (!INIT && !act) return;
-    const int64_t v0 = (int64_t)blockIdx.x * g.per * nsub + sub;
-    for (int j = 0; j < g.per; ++j) {
-        const int64_t v = v0 + (int64_t)j * nsub;
-        if (v >= V) break;
-        const int b = var_ptr[v], e = var_ptr[v + 1];
-        double p = ld_msg<NT>(&lappr[(size_t)v * ld + f]);
-        if (INIT) {
-            if (act && e > b) p = p + 0.0;
-        } else {
-            for (int k = b; k < e; ++k) p += ld_msg<NT>(&c2v[(size_t)var_edge[k] * ld + f]);
-        }
-        post[(size_t)v * ld + f] = p;
-    }
+    if (MODE != kFirst && bad) a.unsat[f] = 1;
 }
 
 __global__ void k_init_status(int B, int ld, uint8_t *active, uint8_t *success, int32_t *iters) {
@@ -202,13 +248,13 @@ __global__ void k_init_status(int B, int ld, uint8_t *active, uint8_t *success, 
     }
 }
 
-// Frames whose posterior after sweep t satisfies the syndrome stop with
+// Frames in [f0, f1) whose posterior after sweep t satisfies the syndrome stop with
 // (success=1, iterations=t) (decoder.pyx:431-433, :402-405 for t = 0).  On the
 // final call every still-active frame stops with (0, max_iterations) (:435-436).
-__global__ void k_status(int B, int t, int final_call, int32_t final_iters, const uint8_t *__restrict__ unsat_t,
-                         uint8_t *active, uint8_t *success, int32_t *iters) {
-    const int f = blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= B || !active[f]) return;
+__global__ void k_status(int f0, int f1, int t, int final_call, int32_t final_iters,
+                         const uint8_t *__restrict__ unsat_t, uint8_t *active, uint8_t *success, int32_t *iters) {
+    const int f = f0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= f1 || !active[f]) return;
     if (!unsat_t[f]) {
         success[f] = 1;
         iters[f] = t;
@@ -246,82 +292,211 @@ static DecodeWs carve(const qr_code *code, int ld, void *base) {
 
 // Runtime tuning knobs (qr_tune_set); defaults picked by scripts/tune.py on MI355X.
 struct Tuning {
-    std::atomic<int> check_ft{256}, check_per{4}, var_ft{256}, var_per{4}, nt{1};
+    std::atomic<int> check_ft{256}, check_per{4}, var_ft{256}, var_per{4}, nt{1}, split{2};
 };
 static Tuning g_tune;
 
-static Geom make_geom(int ld, int ft_req, int per) {
+static Geom make_geom(int ncols, int ft_req, int per) {
     int ft = 256;
-    while (ft > 64 && (ft > ft_req || ld % ft)) ft >>= 1;
+    while (ft > 64 && (ft > ft_req || ncols % ft)) ft >>= 1;
     int lft = 6;
     while ((1 << lft) < ft) ++lft;
     return Geom{lft, per < 1 ? 1 : per};
 }
 
+// Everything one decode call needs to issue its launches.
+struct Plan {
+    const qr_code *code;
+    int B, ld;
+    const double *lappr;
+    const uint8_t *synd;
+    double *post;
+    uint8_t *success;
+    int32_t *iters;
+    DecodeWs w;
+    bool nt;
+    hipStream_t s;
+
+    CheckArgs check_args(const DegreeClass &cls, const double *post_in, uint8_t *unsat, int f0, int f1) const {
+        CheckArgs a;
+        a.checks = cls.d_checks;
+        a.n_checks = cls.n;
+        a.chk_ptr = code->d_chk_ptr;
+        a.chk_edge = code->d_chk_edge;
+        a.chk_var = code->d_chk_var;
+        a.post = post_in;
+        a.c2v = w.c2v;
+        a.synd = synd;
+        a.active = w.active;
+        a.unsat = unsat;
+        a.ld = ld;
+        a.f_off = f0;
+        a.g = make_geom(f1 - f0, g_tune.check_ft.load(), g_tune.check_per.load());
+        const int64_t per_block = (int64_t)a.g.per * (256 >> a.g.lft);
+        a.nbx = (unsigned)((cls.n + per_block - 1) / per_block);
+        a.gtab = code->d_mtab;
+        return a;
+    }
+    VarArgs var_args(int f0, int f1) const {
+        VarArgs a;
+        a.V = code->V;
+        a.var_ptr = code->d_var_ptr;
+        a.var_edge = code->d_var_edge;
+        a.lappr = lappr;
+        a.c2v = w.c2v;
+        a.post = post;
+        a.active = w.active;
+        a.ld = ld;
+        a.f_off = f0;
+        a.g = make_geom(f1 - f0, g_tune.var_ft.load(), g_tune.var_per.load());
+        const int64_t per_block = (int64_t)a.g.per * (256 >> a.g.lft);
+        a.nbx = (unsigned)((code->V + per_block - 1) / per_block);
+        return a;
+    }
+};
+
+// Dispatch a templated launch on the check degree (2..16); `handled` is false otherwise.
+#define QR_DEG_SWITCH(DEG, CASE, handled)                                                                    \
+    switch (DEG) {                                                                                           \
+        CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) \
+        CASE(14) CASE(15) CASE(16)                                                                           \
+        default: handled = false;                                                                            \
+    }
+
 template <int MODE, bool NT>
-static int launch_check_class(const qr_code *code, const DegreeClass &cls, int ld, const double *post, double *c2v,
-                              const uint8_t *synd, const uint8_t *active, uint8_t *unsat, hipStream_t s) {
-    const Geom g = make_geom(ld, g_tune.check_ft.load(), g_tune.check_per.load());
-    const int64_t per_block = (int64_t)g.per * (256 >> g.lft);
-    dim3 grid((unsigned)((cls.n + per_block - 1) / per_block), (unsigned)(ld >> g.lft));
+static int launch_check_class(const Plan &P, const DegreeClass &cls, const double *post_in, uint8_t *unsat, int f0,
+                              int f1) {
+    const CheckArgs a = P.check_args(cls, post_in, unsat, f0, f1);
+    dim3 grid(a.nbx, (unsigned)((f1 - f0) >> a.g.lft));
     ProfScope ps(profiling_on() ? std::string(MODE == kParityOnly ? "parity_d" : MODE == kFirst ? "check1_d" : "check_d") +
                                       std::to_string(cls.degree)
                                 : std::string(),
-                 s);
-#define QR_CASE(DD)                                                                                          \
-    case DD:                                                                                                 \
-        k_check<DD, MODE, NT><<<grid, 256, 0, s>>>(cls.d_checks, cls.n, g, code->d_chk_ptr, code->d_chk_edge, \
-                                                   code->d_chk_var, post, c2v, synd, active, unsat, ld,        \
-                                                   code->d_mtab);                                             \
+                 P.s);
+#define QR_CASE(DD)                                          \
+    case DD:                                                 \
+        k_check<DD, MODE, NT><<<grid, 256, 0, P.s>>>(a);     \
         break;
-    switch (cls.degree) {
-        QR_CASE(2) QR_CASE(3) QR_CASE(4) QR_CASE(5) QR_CASE(6) QR_CASE(7) QR_CASE(8) QR_CASE(9) QR_CASE(10)
-        QR_CASE(11) QR_CASE(12) QR_CASE(13) QR_CASE(14) QR_CASE(15) QR_CASE(16)
-        default:
-            k_check_generic<MODE><<<grid, 256, 0, s>>>(cls.d_checks, cls.n, g, code->d_chk_ptr, code->d_chk_edge,
-                                                       code->d_chk_var, post, c2v, synd, active, unsat, ld,
-                                                       code->d_mtab);
-    }
+    bool handled = true;
+    QR_DEG_SWITCH(cls.degree, QR_CASE, handled)
 #undef QR_CASE
+    if (!handled) k_check_generic<MODE><<<grid, 256, 0, P.s>>>(a);
     QR_LAUNCH_CHECK();
     return QR_OK;
 }
 
+// Check sweep of frames [f0, f1) over every degree class except `skip` (index or -1).
 template <int MODE>
-static int launch_check_all(const qr_code *code, int ld, const double *post, double *c2v, const uint8_t *synd,
-                            const uint8_t *active, uint8_t *unsat, hipStream_t s) {
-    ProfScope ps(MODE == kParityOnly ? "parity" : MODE == kFirst ? "check1" : "check", s);
-    const bool nt = g_tune.nt.load() != 0;
-    for (const auto &cls : code->classes) {
-        int rc = nt ? launch_check_class<MODE, true>(code, cls, ld, post, c2v, synd, active, unsat, s)
-                    : launch_check_class<MODE, false>(code, cls, ld, post, c2v, synd, active, unsat, s);
+static int launch_checks(const Plan &P, const double *post_in, uint8_t *unsat, int f0, int f1, int skip = -1) {
+    for (int k = 0; k < (int)P.code->classes.size(); ++k) {
+        if (k == skip) continue;
+        const DegreeClass &cls = P.code->classes[k];
+        int rc = P.nt ? launch_check_class<MODE, true>(P, cls, post_in, unsat, f0, f1)
+                      : launch_check_class<MODE, false>(P, cls, post_in, unsat, f0, f1);
         if (rc) return rc;
     }
     return QR_OK;
 }
 
 template <bool INIT>
-static int launch_var(const qr_code *code, int ld, const double *lappr, const double *c2v, double *post,
-                      const uint8_t *active, hipStream_t s) {
-    ProfScope ps(INIT ? "var_init" : "var", s);
-    const Geom g = make_geom(ld, g_tune.var_ft.load(), g_tune.var_per.load());
-    const int64_t per_block = (int64_t)g.per * (256 >> g.lft);
-    dim3 grid((unsigned)((code->V + per_block - 1) / per_block), (unsigned)(ld >> g.lft));
-    if (g_tune.nt.load())
-        k_var<INIT, true><<<grid, 256, 0, s>>>(code->V, g, code->d_var_ptr, code->d_var_edge, lappr, c2v, post,
-                                               active, ld);
-    else
-        k_var<INIT, false><<<grid, 256, 0, s>>>(code->V, g, code->d_var_ptr, code->d_var_edge, lappr, c2v, post,
-                                                active, ld);
+static int launch_var(const Plan &P, int f0, int f1) {
+    ProfScope ps(INIT ? "var_init" : "var", P.s);
+    const VarArgs a = P.var_args(f0, f1);
+    dim3 grid(a.nbx, (unsigned)((f1 - f0) >> a.g.lft));
+    if (P.nt) k_var<INIT, true><<<grid, 256, 0, P.s>>>(a);
+    else k_var<INIT, false><<<grid, 256, 0, P.s>>>(a);
     QR_LAUNCH_CHECK();
     return QR_OK;
 }
 
-static int launch_status(int B, int ld, int t, int final_call, int32_t final_iters, const uint8_t *unsat_t,
-                         uint8_t *active, uint8_t *success, int32_t *iters, hipStream_t s) {
-    ProfScope ps("status", s);
-    k_status<<<(B + 255) / 256, 256, 0, s>>>(B, t, final_call, final_iters, unsat_t, active, success, iters);
+template <int MODE, bool NT>
+static int launch_fused_nt(const Plan &P, const DegreeClass &cls, uint8_t *unsat, int cf0, int cf1, int vf0, int vf1) {
+    const CheckArgs ca = P.check_args(cls, P.post, unsat, cf0, cf1);
+    const VarArgs va = P.var_args(vf0, vf1);
+    const unsigned nbc = ca.nbx * (unsigned)((cf1 - cf0) >> ca.g.lft);
+    const unsigned nbv = va.nbx * (unsigned)((vf1 - vf0) >> va.g.lft);
+    ProfScope ps(profiling_on() ? std::string("fused_d") + std::to_string(cls.degree) : std::string(), P.s);
+#define QR_CASE(DD)                                                                 \
+    case DD:                                                                        \
+        k_fused<DD, MODE, NT><<<nbc + nbv, 256, 0, P.s>>>(ca, va, nbc, nbc + nbv); \
+        break;
+    bool handled = true;
+    QR_DEG_SWITCH(cls.degree, QR_CASE, handled)
+#undef QR_CASE
+    if (!handled) return set_error(QR_EUNSUPPORTED, "fused launch needs check degree <= 16");
     QR_LAUNCH_CHECK();
+    return QR_OK;
+}
+
+template <int MODE>
+static int launch_fused(const Plan &P, const DegreeClass &cls, uint8_t *unsat, int cf0, int cf1, int vf0, int vf1) {
+    return P.nt ? launch_fused_nt<MODE, true>(P, cls, unsat, cf0, cf1, vf0, vf1)
+                : launch_fused_nt<MODE, false>(P, cls, unsat, cf0, cf1, vf0, vf1);
+}
+
+static int launch_status(const Plan &P, int f0, int f1, int t, int final_call, int32_t final_iters,
+                         const uint8_t *unsat_t) {
+    ProfScope ps("status", P.s);
+    f1 = std::min(f1, P.B);
+    if (f1 <= f0) return QR_OK;
+    k_status<<<(f1 - f0 + 255) / 256, 256, 0, P.s>>>(f0, f1, t, final_call, final_iters, unsat_t, P.w.active,
+                                                     P.success, P.iters);
+    QR_LAUNCH_CHECK();
+    return QR_OK;
+}
+
+// Flooding schedule, all frames in lock-step (decoder.pyx:424-433).
+static int run_flat(const Plan &P, int max_it) {
+    const int ld = P.ld;
+    int rc;
+    for (int t = 1; t <= max_it; ++t) {
+        uint8_t *unsat_prev = P.w.unsat + (size_t)(t - 1) * ld;
+        if (t == 1) {
+            if ((rc = launch_checks<kFirst>(P, P.post, unsat_prev, 0, ld))) return rc;
+        } else {
+            if ((rc = launch_checks<kNormal>(P, P.post, unsat_prev, 0, ld))) return rc;
+            if ((rc = launch_status(P, 0, ld, t - 1, 0, 0, unsat_prev))) return rc;
+        }
+        if ((rc = launch_var<false>(P, 0, ld))) return rc;
+    }
+    return QR_OK;
+}
+
+// The same per-frame schedule with the batch split in two frame halves A | B
+// whose sweeps are software-pipelined half an iteration apart:
+//   C_A(1); for t: [V_A(t) | C_B(t)], S_B(t-1), [C_A(t+1) | V_B(t)], S_A(t)
+// C = check sweep (+ parity of the previous posteriors), S = status update,
+// V = variable sweep, [x | y] = one k_fused launch.  Per frame the order
+// C(t) -> S(t-1) -> V(t) -> C(t+1) is exactly that of run_flat.
+static int run_split(const Plan &P, int max_it) {
+    const int ld = P.ld, h = ld / 2;
+    const int A0 = 0, A1 = h, B0 = h, B1 = ld;
+    int big = 0;
+    for (int k = 1; k < (int)P.code->classes.size(); ++k)
+        if (P.code->classes[k].n > P.code->classes[big].n) big = k;
+    const DegreeClass &cls = P.code->classes[big];
+    auto row = [&](int t) { return P.w.unsat + (size_t)t * ld; };
+    int rc;
+    // C_A(1)
+    if ((rc = launch_checks<kFirst>(P, P.post, row(0), A0, A1))) return rc;
+    for (int t = 1; t <= max_it; ++t) {
+        // [V_A(t) | C_B(t)]   (the other degree classes of C_B(t) as plain launches)
+        if (t == 1) {
+            if ((rc = launch_checks<kFirst>(P, P.post, row(0), B0, B1, big))) return rc;
+            if ((rc = launch_fused<kFirst>(P, cls, row(0), B0, B1, A0, A1))) return rc;
+        } else {
+            if ((rc = launch_checks<kNormal>(P, P.post, row(t - 1), B0, B1, big))) return rc;
+            if ((rc = launch_fused<kNormal>(P, cls, row(t - 1), B0, B1, A0, A1))) return rc;
+            if ((rc = launch_status(P, B0, B1, t - 1, 0, 0, row(t - 1)))) return rc;
+        }
+        if (t < max_it) {
+            // [C_A(t+1) | V_B(t)]
+            if ((rc = launch_checks<kNormal>(P, P.post, row(t), A0, A1, big))) return rc;
+            if ((rc = launch_fused<kNormal>(P, cls, row(t), A0, A1, B0, B1))) return rc;
+            if ((rc = launch_status(P, A0, A1, t, 0, 0, row(t)))) return rc;
+        } else {
+            if ((rc = launch_var<false>(P, B0, B1))) return rc;
+        }
+    }
     return QR_OK;
 }
 
@@ -335,38 +510,31 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     if (ws_size < ws_bytes(code, ld, max_it))
         return set_error(QR_EVALUE, "decode: workspace too small (%zu < %zu)", ws_size, ws_bytes(code, ld, max_it));
     DeviceGuard dg(code->device);
-    DecodeWs w = carve(code, ld, ws_ptr);
+    Plan P{code, B, ld, lappr, synd, final_post, success, iters, carve(code, ld, ws_ptr), g_tune.nt.load() != 0, s};
     const int rows = (max_it > 0 ? max_it : 0) + 2;
     int rc;
-    QR_HIP(hipMemsetAsync(w.unsat, 0, (size_t)rows * ld, s));
-    k_init_status<<<(ld + 255) / 256, 256, 0, s>>>(B, ld, w.active, success, iters);
+    QR_HIP(hipMemsetAsync(P.w.unsat, 0, (size_t)rows * ld, s));
+    k_init_status<<<(ld + 255) / 256, 256, 0, s>>>(B, ld, P.w.active, success, iters);
     QR_LAUNCH_CHECK();
     // decoder.pyx:400-405: the input itself may already satisfy the syndrome.
-    if ((rc = launch_check_all<kParityOnly>(code, ld, lappr, nullptr, synd, w.active, w.unsat, s))) return rc;
-    if ((rc = launch_status(B, ld, 0, 0, 0, w.unsat, w.active, success, iters, s))) return rc;
+    if ((rc = launch_checks<kParityOnly>(P, lappr, P.w.unsat, 0, ld))) return rc;
+    if ((rc = launch_status(P, 0, ld, 0, 0, 0, P.w.unsat))) return rc;
     // decoder.pyx:408-421: c2v = 0, first variable sweep.
-    if ((rc = launch_var<true>(code, ld, lappr, nullptr, final_post, w.active, s))) return rc;
-    for (int t = 1; t <= max_it; ++t) {
-        uint8_t *unsat_prev = w.unsat + (size_t)(t - 1) * ld;
-        if (t == 1) {
-            if ((rc = launch_check_all<kFirst>(code, ld, final_post, w.c2v, synd, w.active, unsat_prev, s))) return rc;
-        } else {
-            if ((rc = launch_check_all<kNormal>(code, ld, final_post, w.c2v, synd, w.active, unsat_prev, s))) return rc;
-            if ((rc = launch_status(B, ld, t - 1, 0, 0, unsat_prev, w.active, success, iters, s))) return rc;
-        }
-        if ((rc = launch_var<false>(code, ld, lappr, w.c2v, final_post, w.active, s))) return rc;
-    }
+    if ((rc = launch_var<true>(P, 0, ld))) return rc;
+    int max_deg = 0;
+    for (const auto &c : code->classes) max_deg = std::max(max_deg, c.degree);
+    const bool split = g_tune.split.load() >= 2 && ld % 512 == 0 && max_deg <= 16;
+    if ((rc = split ? run_split(P, max_it) : run_flat(P, max_it))) return rc;
     // Check after the last sweep; then every frame still running stops with (0, max).
     const int tf = max_it > 0 ? max_it : 0;
-    uint8_t *unsat_last = w.unsat + (size_t)tf * ld;
+    uint8_t *unsat_last = P.w.unsat + (size_t)tf * ld;
     if (max_it > 0) {
-        if ((rc = launch_check_all<kParityOnly>(code, ld, final_post, nullptr, synd, w.active, unsat_last, s)))
-            return rc;
+        if ((rc = launch_checks<kParityOnly>(P, final_post, unsat_last, 0, ld))) return rc;
     } else {
         // decoder.pyx:424 with max_iterations <= 0: no sweep, no check -> (0, max_iterations)
         QR_HIP(hipMemsetAsync(unsat_last, 1, (size_t)ld, s));
     }
-    if ((rc = launch_status(B, ld, tf, 1, max_it, unsat_last, w.active, success, iters, s))) return rc;
+    if ((rc = launch_status(P, 0, ld, tf, 1, max_it, unsat_last))) return rc;
     return QR_OK;
 }
 
@@ -540,7 +708,7 @@ int qr_tune_set(const char *name, int64_t value) {
     const std::string n = name ? name : "";
     std::atomic<int> *k = n == "check_ft" ? &g_tune.check_ft : n == "check_per" ? &g_tune.check_per
                         : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
-                        : n == "nt"       ? &g_tune.nt       : nullptr;
+                        : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split : nullptr;
     if (!k) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     if (value < 0 || value > 4096) return set_error(QR_EVALUE, "tuning value out of range");
     k->store((int)value);
@@ -551,7 +719,7 @@ int qr_tune_get(const char *name, int64_t *value) {
     const std::string n = name ? name : "";
     const std::atomic<int> *k = n == "check_ft" ? &g_tune.check_ft : n == "check_per" ? &g_tune.check_per
                               : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
-                              : n == "nt"       ? &g_tune.nt       : nullptr;
+                              : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split : nullptr;
     if (!k || !value) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     *value = k->load();
     return QR_OK;

@@ -95,6 +95,10 @@ def load():
         fn.argtypes = args
         fn.restype = _RESTYPE.get(name, C.c_int)
     _lib = L
+    # QAMR_TUNE="knob=value,knob=value" presets the kernel-geometry knobs (qr_tune_set).
+    for item in filter(None, os.environ.get("QAMR_TUNE", "").split(",")):
+        k, v = item.split("=")
+        check(L.qr_tune_set(k.strip().encode(), int(v)), "QAMR_TUNE")
     return L
 
 

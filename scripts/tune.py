@@ -20,8 +20,8 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--iters", type=int, default=6)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--grid", default="check_ft=64,128,256;check_per=1,2,4,8;nt=0,1")
-    ap.add_argument("--var-grid", default="var_ft=64,256;var_per=1,4,8")
+    ap.add_argument("--grid", default="split=1,2;check_per=2,4,8;nt=0,1")
+    ap.add_argument("--var-grid", default="split=2;var_per=2,4,8;check_ft=128,256")
     args = ap.parse_args()
     import torch
     import qamr
@@ -55,13 +55,22 @@ def main():
         for cfg in configs + vconfigs:
             for k, v in cfg.items():
                 _lib.tune_set(k, v)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            pipe.decode(lap, b, fin, su, it)
+            e1.record()
+            torch.cuda.synchronize()
+            wall = e0.elapsed_time(e1)
             qamr.profile_reset()
             qamr.profile_enable(True)
             pipe.decode(lap, b, fin, su, it)
             torch.cuda.synchronize()
             qamr.profile_enable(False)
             key = json.dumps(cfg, sort_keys=True)
-            rec = results.setdefault(key, {"check_d7": [], "var": []})
+            rec = results.setdefault(key, {"check_d7": [], "var": [], "wall": [], "fused": []})
+            rec["wall"].append(wall / args.iters)
+            ms, n = qamr.profile_query("fused_d7")
+            rec["fused"].append(ms / max(n, 1))
             ms, n = qamr.profile_query("check_d7")
             rec["check_d7"].append(ms / max(n, 1))
             ms, n = qamr.profile_query("var")
@@ -73,14 +82,15 @@ def main():
             elif h != ref:
                 print("MISMATCH", cfg, h, ref, flush=True)
             for k in cfg:
-                _lib.tune_set(k, {"check_ft": 256, "check_per": 4, "var_ft": 256, "var_per": 4, "nt": 1}[k])
+                _lib.tune_set(k, {"check_ft": 256, "check_per": 4, "var_ft": 256, "var_per": 4, "nt": 1,
+                                  "split": 2}[k])
     rows = []
     for key, rec in results.items():
-        rows.append((min(rec["check_d7"]), min(rec["var"]), key))
+        rows.append((min(rec["wall"]), min(rec["check_d7"]), min(rec["var"]), min(rec["fused"]), key))
     rows.sort()
-    print(f"{'check_d7 ms':>12} {'var ms':>9}  config")
-    for c, v, k in rows:
-        print(f"{c:12.3f} {v:9.3f}  {k}")
+    print(f"{'ms/iter':>8} {'check_d7':>9} {'var':>7} {'fused_d7':>9}  config   (kernel columns: ms per launch)")
+    for w, c, v, fu, k in rows:
+        print(f"{w:8.3f} {c:9.3f} {v:7.3f} {fu:9.3f}  {k}")
 
 
 if __name__ == "__main__":
