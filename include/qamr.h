@@ -161,6 +161,18 @@ QR_API int qr_bob_map_device(const qr_demap *dm, int32_t B, int32_t ld, int64_t 
  * d_nhat[s][f] = g(d_y[s][f], d_index[s][f]) (noisemapper.pyx:289-292). */
 QR_API int qr_map_noise_device(const qr_demap *dm, int32_t B, int32_t ld, int64_t S, const double *d_y,
                                const int64_t *d_index, double *d_nhat, void *stream);
+/* PAMAlphabet.demap_symbols_to_bits (alphabet.pyx:98-107): d_x[S][ld] -> d_word[S*bps][ld]
+ * (padding frames f in [B, ld) get the bits of symbol 0). */
+QR_API int qr_symbols_to_bits_device(int32_t bit_per_symbol, int32_t B, int32_t ld, int64_t S, const int64_t *d_x,
+                                     uint8_t *d_word, void *stream);
+/* Direct reconciliation LAPPRs (sims/reconciliation.pyx:25-51, _y_to_lappr_grey):
+ * d_y[S][ld] -> d_lappr[S*bps][ld], two_variance = 2 * noise variance. */
+QR_API int qr_direct_lappr_device(const qr_demap *dm, double two_variance, int32_t B, int32_t ld, int64_t S,
+                                  const double *d_y, double *d_lappr, void *stream);
+/* Hard reverse reconciliation LAPPRs (noisemapper.pyx:423-432, bare_llr):
+ * d_lappr[(s*bps+k)][f] = d_table[x * bps + k] with the device table[M][bps]. */
+QR_API int qr_bare_llr_device(int32_t bit_per_symbol, const double *d_table, int32_t B, int32_t ld, int64_t S,
+                              const int64_t *d_x, double *d_lappr, void *stream);
 /* Matrix.eval_syndrome (matrix.pyx:55-60): d_word[V][ld] -> d_synd[C][ld]. */
 QR_API int qr_syndrome_device(const qr_code *code, int32_t B, int32_t ld, const uint8_t *d_word, uint8_t *d_synd,
                        void *stream);

@@ -62,6 +62,65 @@ __global__ void __launch_bounds__(256) k_bob(const DemapTables *__restrict__ tab
     for (int k = 0; k < t.bps; ++k) word[(s * t.bps + k) * ld + f] = (uint8_t)((gray >> k) & 1);
 }
 
+// Direct reconciliation (sims/reconciliation.pyx:25-51, _y_to_lappr_grey): Bob's
+// BICM LAPPRs of his own sample y, Gray-labelled log-sums over the alphabet.
+// (y - a_i)**2 is evaluated as a product (the reference's pow(x, 2.0)).
+__global__ void __launch_bounds__(256) k_direct_lappr(const DemapTables *__restrict__ tab, double two_var, int B,
+                                                      int ld, int64_t S, const double *__restrict__ y,
+                                                      double *__restrict__ lappr) {
+    const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t s = item / ld;
+    const int f = (int)(item - s * ld);
+    if (s >= S || f >= B) return;
+    const DemapTables &t = *tab;
+    const double yv = y[s * ld + f];
+    double N[kMaxBps], D[kMaxBps];
+#pragma unroll
+    for (int k = 0; k < kMaxBps; ++k) { N[k] = 0; D[k] = 0; }
+    for (int i = 0; i < t.M; ++i) {
+        const double d = yv - t.a[i];
+        const double add = exp(-(d * d) / two_var);
+        int mi = i;
+#pragma unroll
+        for (int k = 0; k < kMaxBps; ++k) {
+            if (k < t.bps) {
+                if ((mi * (mi + 1)) & 3) D[k] += add;
+                else                     N[k] += add;
+                mi >>= 1;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxBps; ++k)
+        if (k < t.bps) lappr[(s * t.bps + k) * ld + f] = log(N[k]) - log(D[k]);
+}
+
+// Hard reverse reconciliation (noisemapper.pyx:423-432, bare_llr): Alice's LAPPRs
+// are the table row of her own symbol, table[M][bps] built on the host (:197-220).
+__global__ void __launch_bounds__(256) k_bare_llr(const double *__restrict__ table, int M, int bps, int B, int ld,
+                                                  int64_t S, const int64_t *__restrict__ x,
+                                                  double *__restrict__ lappr) {
+    const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t s = item / ld;
+    const int f = (int)(item - s * ld);
+    if (s >= S || f >= B) return;
+    const int64_t xi = x[s * ld + f];
+    const bool ok = xi >= 0 && xi < M;
+    for (int k = 0; k < bps; ++k) lappr[(s * bps + k) * ld + f] = ok ? table[xi * bps + k] : __builtin_nan("");
+}
+
+// alphabet.pyx:98-107 with the reflected Gray table of bicm.pyx:26-41.
+__global__ void __launch_bounds__(256) k_symbols_to_bits(int bps, int B, int ld, int64_t S,
+                                                         const int64_t *__restrict__ x, uint8_t *__restrict__ word) {
+    const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t s = item / ld;
+    const int f = (int)(item - s * ld);
+    if (s >= S || f >= ld) return;
+    const int64_t xi = (f < B) ? x[s * ld + f] : 0;
+    const int64_t g = xi ^ (xi >> 1);
+    for (int k = 0; k < bps; ++k) word[(s * bps + k) * ld + f] = (uint8_t)((g >> k) & 1);
+}
+
 // noisemapper.pyx:289-292, :373-388 with a caller-given index (x_hat).
 __global__ void __launch_bounds__(256) k_map_noise(const DemapTables *__restrict__ tab, int B, int ld, int64_t S,
                                                    const double *__restrict__ y, const int64_t *__restrict__ idx,
@@ -283,6 +342,44 @@ int qr_map_noise_device(const qr_demap *dm, int32_t B, int32_t ld, int64_t S, co
     hipStream_t s = (hipStream_t)stream;
     const int64_t items = S * ld;
     k_map_noise<<<(unsigned)((items + 255) / 256), 256, 0, s>>>(dm->d_tables, B, ld, S, d_y, d_index, d_nhat);
+    QR_LAUNCH_CHECK();
+    return QR_OK;
+}
+
+int qr_direct_lappr_device(const qr_demap *dm, double two_variance, int32_t B, int32_t ld, int64_t S,
+                           const double *d_y, double *d_lappr, void *stream) {
+    if (!dm) return set_error(QR_EVALUE, "null demapper");
+    int rc = check_shape(B, ld, S);
+    if (rc) return rc;
+    DeviceGuard g(dm->device);
+    hipStream_t s = (hipStream_t)stream;
+    ProfScope ps("direct_lappr", s);
+    const int64_t items = S * ld;
+    k_direct_lappr<<<(unsigned)((items + 255) / 256), 256, 0, s>>>(dm->d_tables, two_variance, B, ld, S, d_y, d_lappr);
+    QR_LAUNCH_CHECK();
+    return QR_OK;
+}
+
+int qr_bare_llr_device(int32_t bps, const double *d_table, int32_t B, int32_t ld, int64_t S, const int64_t *d_x,
+                       double *d_lappr, void *stream) {
+    if (bps < 1 || bps > kMaxBps) return set_error(QR_EVALUE, "bit_per_symbol out of range");
+    int rc = check_shape(B, ld, S);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t items = S * ld;
+    k_bare_llr<<<(unsigned)((items + 255) / 256), 256, 0, s>>>(d_table, 1 << bps, bps, B, ld, S, d_x, d_lappr);
+    QR_LAUNCH_CHECK();
+    return QR_OK;
+}
+
+int qr_symbols_to_bits_device(int32_t bps, int32_t B, int32_t ld, int64_t S, const int64_t *d_x, uint8_t *d_word,
+                              void *stream) {
+    if (bps < 1 || bps > kMaxBps) return set_error(QR_EVALUE, "bit_per_symbol out of range");
+    int rc = check_shape(B, ld, S);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t items = S * ld;
+    k_symbols_to_bits<<<(unsigned)((items + 255) / 256), 256, 0, s>>>(bps, B, ld, S, d_x, d_word);
     QR_LAUNCH_CHECK();
     return QR_OK;
 }

@@ -52,6 +52,9 @@ SIGNATURES = {
     "qr_bob_map_device": [vp, i32, i32, i64, vp, vp, vp, vp, vp],
     "qr_map_noise_device": [vp, i32, i32, i64, vp, vp, vp, vp],
     "qr_syndrome_device": [vp, i32, i32, vp, vp, vp],
+    "qr_symbols_to_bits_device": [i32, i32, i32, i64, vp, vp, vp],
+    "qr_direct_lappr_device": [vp, f64, i32, i32, i64, vp, vp, vp],
+    "qr_bare_llr_device": [i32, vp, i32, i32, i64, vp, vp, vp],
     "qr_count_errors_device": [i32, i32, i64, vp, vp, vp, vp, vp, vp, vp],
     "qr_to_frame_innermost_f64": [i32, i32, i64, vp, vp, vp],
     "qr_to_frame_major_f64": [i32, i32, i64, vp, vp, vp],

@@ -25,6 +25,49 @@ from ._lib import check, ptr
 from .alphabet import PAMAlphabet
 
 
+def host_tables(a, th, p, sigma, bps):
+    """The O(M^2) host tables of NoiseMapper.__cinit__ (noisemapper.pyx:166-235),
+    with C erf/log semantics: (fwrd_transition_probability, back_transition_probability,
+    bare_llr_table, inf_erf_table)."""
+    M = len(a)
+    tmp = math.sqrt(2) * sigma
+    fw = np.empty((M, M))
+    for j in range(M):
+        fw[j, 0] = 0.5 * (math.erf((th[1] - a[j]) / tmp) + 1)
+        fw[j, M - 1] = 0.5 * (1 - math.erf((th[M - 1] - a[j]) / tmp))
+        for i in range(1, M - 1):
+            fw[j, i] = 0.5 * (math.erf((th[i + 1] - a[j]) / tmp) - math.erf((th[i] - a[j]) / tmp))
+    back = np.empty((M, M))
+    for i in range(M):
+        for j in range(M):
+            t = 0.0
+            for k in range(M):
+                t += p[k] * fw[k, i]
+            back[i, j] = p[j] * fw[j, i] / t
+    bare = np.empty((M, bps))
+    old = np.seterr(divide="ignore")
+    try:
+        for j in range(M):
+            for k in range(bps):
+                N = D = 0.0
+                for i in range(M):
+                    mi = i >> k
+                    if (mi * (mi + 1)) & 3:
+                        D += fw[j, i]
+                    else:
+                        N += fw[j, i]
+                # C log semantics (log(0) = -inf) rather than math.log's ValueError
+                bare[j, k] = 1e300 if D == 0 else float(np.log(np.float64(N) / np.float64(D)))
+    finally:
+        np.seterr(**old)
+    ierf = np.empty((M, M))
+    for j in range(M):
+        ierf[0, j] = -1
+        for i in range(1, M):
+            ierf[i, j] = math.erf((th[i] - a[j]) / tmp)
+    return fw, back, bare, ierf
+
+
 class NoiseMapper:
     def __init__(self, pa: PAMAlphabet, noise_var: float, sign_config=None, trunkation_threshold: float = 1e-21,
                  n_intervals_per_step: int = 1000, device: int = 0):
@@ -78,46 +121,9 @@ class NoiseMapper:
 
     # ------------------------------------------------- small host-side tables
     def _host_tables(self):
-        """noisemapper.pyx:166-235 (libc erf, as in the reference)."""
-        M = self.order
-        tmp = math.sqrt(2) * self.noise_sigma
-        a, th, p = self.constellation, self.thresholds, self.probabilities
-        fw = np.empty((M, M))
-        for j in range(M):
-            fw[j, 0] = 0.5 * (math.erf((th[1] - a[j]) / tmp) + 1)
-            fw[j, M - 1] = 0.5 * (1 - math.erf((th[M - 1] - a[j]) / tmp))
-            for i in range(1, M - 1):
-                fw[j, i] = 0.5 * (math.erf((th[i + 1] - a[j]) / tmp) - math.erf((th[i] - a[j]) / tmp))
-        back = np.empty((M, M))
-        for i in range(M):
-            for j in range(M):
-                t = 0.0
-                for k in range(M):
-                    t += p[k] * fw[k, i]
-                back[i, j] = p[j] * fw[j, i] / t
-        bare = np.empty((M, self.bit_per_symbol))
-        old = np.seterr(divide="ignore")
-        for j in range(M):
-            for k in range(self.bit_per_symbol):
-                N = D = 0.0
-                for i in range(M):
-                    mi = i >> k
-                    if (mi * (mi + 1)) & 3:
-                        D += fw[j, i]
-                    else:
-                        N += fw[j, i]
-                # C log semantics (log(0) = -inf) rather than math.log's ValueError
-                bare[j, k] = 1e300 if D == 0 else float(np.log(np.float64(N) / np.float64(D)))
-        np.seterr(**old)
-        ierf = np.empty((M, M))
-        for j in range(M):
-            ierf[0, j] = -1
-            for i in range(1, M):
-                ierf[i, j] = math.erf((th[i] - a[j]) / tmp)
-        self.fwrd_transition_probability = fw
-        self.back_transition_probability = back
-        self.bare_llr_table = bare
-        self.inf_erf_table = ierf
+        (self.fwrd_transition_probability, self.back_transition_probability, self.bare_llr_table,
+         self.inf_erf_table) = host_tables(self.constellation, self.thresholds, self.probabilities,
+                                           self.noise_sigma, self.bit_per_symbol)
 
     def _grid(self):
         """Uniform-weighted F_Y on the interpolation grid (noisemapper.pyx:135-144,

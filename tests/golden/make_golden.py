@@ -226,8 +226,37 @@ def gen_pam16_nan():
     np.savez_compressed(os.path.join(HERE, "pam16_25db.npz"), **out)
 
 
+def gen_llr_sources():
+    """Direct-reconciliation LAPPRs (sims/reconciliation.pyx:25-65 via the cpdef
+    y_to_lappr_grey_array) and the NoiseMapper host tables (noisemapper.pyx:166-235)."""
+    from sims.reconciliation import y_to_lappr_grey_array
+
+    out = {}
+    for bps, snrs in ((1, (2.0,)), (2, (3.0, 9.5)), (4, (13.0, 25.0))):
+        pa = PAMAlphabet(bps, 2.0)
+        for snr in snrs:
+            k = f"b{bps}_s{int(10 * snr)}"
+            Es = pa.variance
+            two_var = Es * (10 ** (-snr / 10))
+            nv = two_var / 2
+            rng = np.random.default_rng(77 + bps)
+            x = rng.choice(pa.order, size=200).astype(np.int64)
+            y = np.asarray(pa.index_to_value(x)) + np.sqrt(nv) * rng.standard_normal(200)
+            out[f"{k}_two_var"], out[f"{k}_y"] = two_var, y
+            out[f"{k}_direct"] = np.asarray(y_to_lappr_grey_array(y, pa, two_var))
+            for cfgname, cfg in (("base", None), ("alt", alternating(pa.order))):
+                nm = NoiseMapper(pa, nv, cfg) if cfg is not None else NoiseMapper(pa, nv)
+                out[f"{k}_{cfgname}_fwrd"] = np.asarray(nm.fwrd_transition_probability)
+                out[f"{k}_{cfgname}_back"] = np.asarray(nm.back_transition_probability)
+                out[f"{k}_{cfgname}_bare"] = np.asarray(nm.bare_llr_table)
+                out[f"{k}_{cfgname}_inferf"] = np.asarray(nm.inf_erf_table)
+                out[f"{k}_{cfgname}_bare_llr_x"] = np.asarray(nm.bare_llr(x))
+            out[f"{k}_x"] = x
+    np.savez_compressed(os.path.join(HERE, "llr_sources.npz"), **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["hamming", "node_rules", "reg1008", "demap", "pam16_nan", "dvbs2"]
+    which = sys.argv[1:] or ["hamming", "node_rules", "reg1008", "demap", "pam16_nan", "llr_sources", "dvbs2"]
     for w in which:
         t = time.time()
         print(f"[golden] {w}", flush=True)
