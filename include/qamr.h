@@ -69,7 +69,8 @@ QR_API int qr_profile_query(const char *name, double *total_ms, int64_t *launche
  * nodes per thread, "nt" non-temporal edge-message stream (0/1), "split"
  * (1 = all frames in lock-step, 2 = two frame halves software-pipelined half an
  * iteration apart so each launch overlaps one half's check sweep with the
- * other half's variable sweep). */
+ * other half's variable sweep), "demap_fast" (1 = Newton-located root +
+ * replayed bisection, bit-identical to 0 = the reference's brute-force search). */
 QR_API int qr_tune_set(const char *name, int64_t value);
 QR_API int qr_tune_get(const char *name, int64_t *value);
 

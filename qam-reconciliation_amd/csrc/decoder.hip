@@ -708,7 +708,8 @@ int qr_tune_set(const char *name, int64_t value) {
     const std::string n = name ? name : "";
     std::atomic<int> *k = n == "check_ft" ? &g_tune.check_ft : n == "check_per" ? &g_tune.check_per
                         : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
-                        : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split : nullptr;
+                        : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
+                        : n == "demap_fast" ? &g_demap_fast : nullptr;
     if (!k) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     if (value < 0 || value > 4096) return set_error(QR_EVALUE, "tuning value out of range");
     k->store((int)value);
@@ -719,7 +720,8 @@ int qr_tune_get(const char *name, int64_t *value) {
     const std::string n = name ? name : "";
     const std::atomic<int> *k = n == "check_ft" ? &g_tune.check_ft : n == "check_per" ? &g_tune.check_per
                               : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
-                              : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split : nullptr;
+                              : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
+                              : n == "demap_fast" ? &g_demap_fast : nullptr;
     if (!k || !value) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     *value = k->load();
     return QR_OK;

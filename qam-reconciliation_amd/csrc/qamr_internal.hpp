@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -56,6 +57,8 @@ int launch_transpose_to_fi_f64(int B, int ld, int64_t n, const double *src, doub
 int launch_transpose_to_fm_f64(int B, int ld, int64_t n, const double *src, double *dst, hipStream_t s);
 int launch_transpose_to_fi_u8(int B, int ld, int64_t n, const uint8_t *src, uint8_t *dst, hipStream_t s);
 int launch_transpose_to_fi_i64(int B, int ld, int64_t n, const int64_t *src, int64_t *dst, hipStream_t s);
+
+extern std::atomic<int> g_demap_fast;  // demap.hip (tuning knob "demap_fast")
 
 struct DeviceGuard {
     explicit DeviceGuard(int dev) {

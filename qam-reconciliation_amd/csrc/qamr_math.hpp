@@ -121,52 +121,175 @@ QR_HD double single_F_Y(const DemapTables& t, double y) {
     return res;
 }
 
+// ------------------------------------------------------------------------
+// g_inv_search (noisemapper.pyx:310-345, y_accuracy = 1e-9).
+//
+// The reference brackets the root of F_Y(y) = T by doubling, then bisects to
+// |hi - lo| <= 1e-9: 31..40 evaluations of F_Y (M erf each) per call.  Every
+// decision is a comparison sign(F_Y(y) - T).  F_Y is strictly increasing, so
+// away from the root that sign is sign(y - y*).  The fast path therefore
+//   1. locates y* by safeguarded Newton (F_Y and its density, ~4-6 steps), and
+//   2. replays the reference's bracket + bisection arithmetic exactly (same
+//      lo/hi/mid doubles), deciding each comparison by sign(y - y*) unless y is
+//      within a certified window W of y*, where F_Y(y) is evaluated exactly as
+//      the reference does.  W bounds the Newton error plus the float error of
+//      F_Y (<= (M+2) ulp(1), absolute) divided by the density at y*.
+// The returned doubles are bit-identical to the brute-force search with the
+// same F_Y (tests/test_demap_replay.py checks this over millions of draws);
+// when Newton cannot certify a root (NaN target, T outside (0,1), density
+// underflow, W too wide) the brute-force search runs instead.
+// ------------------------------------------------------------------------
+
 // Iteration cap on the bracket and bisection loops.  The reference loops are
 // unbounded (noisemapper.pyx:323-342); for finite targets they take <= ~1100
 // steps, so the cap only turns a reference hang (T > 1 or |y| > ~4e6) into a
 // NaN instead of a stuck GPU wave.
 constexpr int kSearchCap = 2200;
 
-// noisemapper.pyx:310-345 (y_accuracy = 1e-9 default).
-QR_HD double g_inv_search(const DemapTables& t, double n_hat, int i) {
-    double T;
-    if (t.sign[i]) T = t.Fthr[i + 1] - n_hat * t.dF[i];
-    else           T = n_hat * t.dF[i] + t.Fthr[i];
-    double lo, hi, F;
+// Three-way comparison oracle of the search: sign(F_Y(y) - T).
+struct SearchCmp {
+    const DemapTables *t;
+    double T, ystar, W;
+    bool have;
+    QR_HD int operator()(double y) const {
+        if (have) {
+            const double d = y - ystar;
+            if (d > W) return 1;
+            if (d < -W) return -1;
+        }
+        const double F = single_F_Y(*t, y);
+        return (F > T) ? 1 : (F < T) ? -1 : 0;   // NaN -> 0 (neither > nor <)
+    }
+};
+
+// The reference's bracket + bisection (noisemapper.pyx:314-345) on a comparison oracle.
+QR_HD double search_replay(const SearchCmp &cmp) {
+    double lo, hi;
     int guard = 0;
-    if (T > .5) {
+    if (cmp.T > .5) {
         hi = 1; lo = 0;
-        F = single_F_Y(t, hi);
-        while (F < T) {
+        while (cmp(hi) < 0) {             // while (F_Y(hi) < T)
             if (++guard > kSearchCap) return NAN;
-            lo = hi; hi *= 2.; F = single_F_Y(t, hi);
+            lo = hi; hi *= 2.;
         }
     } else {
         lo = -1; hi = 0;
-        F = single_F_Y(t, lo);
-        while (F > T) {
+        while (cmp(lo) > 0) {             // while (F_Y(lo) > T)
             if (++guard > kSearchCap) return NAN;
-            hi = lo; lo *= 2.; F = single_F_Y(t, lo);
+            hi = lo; lo *= 2.;
         }
     }
     while ((hi - lo) > 1e-9) {
         if (++guard > kSearchCap) return NAN;
         const double mid = (hi + lo) / 2;
-        F = single_F_Y(t, mid);
-        if (F > T) hi = mid; else lo = mid;
+        if (cmp(mid) > 0) hi = mid; else lo = mid;   // if (F_Y(mid) > T) hi = mid else lo = mid
     }
     return (hi + lo) / 2;
 }
 
+QR_HD double search_target(const DemapTables &t, double n_hat, int i) {
+    if (t.sign[i]) return t.Fthr[i + 1] - n_hat * t.dF[i];
+    return n_hat * t.dF[i] + t.Fthr[i];
+}
+
+// Brute force: the reference algorithm verbatim.
+QR_HD double g_inv_search(const DemapTables &t, double n_hat, int i) {
+    SearchCmp cmp{&t, search_target(t, n_hat, i), 0.0, 0.0, false};
+    return search_replay(cmp);
+}
+
+// F_Y(y) and its density f_Y(y) = sum_m p_m exp(-u_m^2) / (sqrt(pi) den), u_m = (y - a_m)/den.
+// Accurate to a few ulp; only steers Newton (never decides a comparison).
+QR_HD void F_and_density(const DemapTables &t, double y, double &F, double &f) {
+    constexpr double kInvSqrtPi = 0.56418958354775628695;
+    double sF = 0.0, sf = 0.0;
+    for (int m = 0; m < t.M; ++m) {
+        const double u = (y - t.a[m]) / t.den;
+        const double au = fabs(u);
+        const double e = exp(-au * au);          // shared by the density and cephes' erfc
+        double r;
+        if (au > 1.0) {
+            double p, q;
+            if (au < 8.0) {
+                p = CephesErf::P[0];
+                for (int i = 1; i <= 8; ++i) p = p * au + CephesErf::P[i];
+                q = au + CephesErf::Q[0];
+                for (int i = 1; i < 8; ++i) q = q * au + CephesErf::Q[i];
+            } else {
+                p = CephesErf::R[0];
+                for (int i = 1; i <= 5; ++i) p = p * au + CephesErf::R[i];
+                q = au + CephesErf::S[0];
+                for (int i = 1; i < 6; ++i) q = q * au + CephesErf::S[i];
+            }
+            r = 1.0 - (e * p) / q;
+        } else {
+            const double z = au * au;
+            double p = CephesErf::T[0];
+            for (int i = 1; i <= 4; ++i) p = p * z + CephesErf::T[i];
+            double q = z + CephesErf::U[0];
+            for (int i = 1; i < 5; ++i) q = q * z + CephesErf::U[i];
+            r = au * p / q;
+        }
+        sF += (0.5 * (1 + ((u < 0.0) ? -r : r))) * t.p[m];
+        sf += e * t.p[m];
+    }
+    F = sF;
+    f = sf * (kInvSqrtPi / t.den);
+}
+
+// Safeguarded Newton for F_Y(y) = T; returns false if no certified root.
+QR_HD bool newton_root(const DemapTables &t, double T, double &ystar, double &W) {
+    if (!(T > 0.0 && T < 1.0)) return false;
+    // bracket from the decision thresholds: F_Y(t_k) = F_Y_thresholds[k]
+    int k = 0;
+    while (k < t.M && !(t.Fthr[k + 1] >= T)) ++k;
+    if (k >= t.M) return false;
+    double lo = t.thr[k], hi = t.thr[k + 1];
+    double y = (k == 0) ? t.a[0] : (k == t.M - 1) ? t.a[t.M - 1] : 0.5 * (lo + hi);
+    if (!(y > lo && y < hi)) y = 0.5 * (lo + hi);
+    double F, f, step = hi - lo;
+    bool conv = false;
+    for (int it = 0; it < 80; ++it) {
+        F_and_density(t, y, F, f);
+        const double g = F - T;
+        if (g > 0) hi = y; else lo = y;
+        double yn = y - g / f;
+        if (!(yn > lo && yn < hi)) yn = 0.5 * (lo + hi);      // bisection fallback (also f == 0 / NaN)
+        step = yn - y;
+        y = yn;
+        if (fabs(step) <= 1e-13 * (fabs(y) + t.den)) { conv = true; break; }
+    }
+    if (!conv) return false;
+    F_and_density(t, y, F, f);
+    if (!(f > 0.0)) return false;
+    // window: Newton residual and last step + float error of F_Y (<= (M+2) ulp(1),
+    // absolute) over the density, with a x8..x16 margin.  Any finite W is correct
+    // (ambiguous comparisons are evaluated exactly); W only sets the cost.
+    const double eps = 2.220446049250313e-16;
+    const double w = 8.0 * fabs(F - T) / f + 4.0 * fabs(step) + 16.0 * (t.M + 4) * eps / f + 8.0 * eps * fabs(y);
+    if (!(w < 1e-3)) return false;
+    ystar = y;
+    W = w;
+    return true;
+}
+
+// Fast g_inv_search: bit-identical to g_inv_search (see the block comment).
+QR_HD double g_inv_search_fast(const DemapTables &t, double n_hat, int i) {
+    SearchCmp cmp{&t, search_target(t, n_hat, i), 0.0, 0.0, false};
+    cmp.have = newton_root(t, cmp.T, cmp.ystar, cmp.W);
+    return search_replay(cmp);
+}
+
 // noisemapper.pyx:450-540 for one symbol; out[k] = LAPPR of Gray bit k (LSB first).
 // Note the reference quirk kept on purpose: no /2sigma^2 for k < j (:503-507).
+template <bool FAST = true>
 QR_HD void demap_symbol(const DemapTables& t, double n, int j, double alpha, double* out) {
     double N[kMaxBps], D[kMaxBps];
 #pragma unroll
     for (int k = 0; k < kMaxBps; ++k) { N[k] = 0; D[k] = 0; }
     const double aj = t.a[j];
     for (int i = 0; i < t.M; ++i) {
-        const double y = g_inv_search(t, n, i);
+        const double y = FAST ? g_inv_search_fast(t, n, i) : g_inv_search(t, n, i);
         double s = 0;
         for (int k = 0; k < j; ++k) s += exp((2 * y - t.a[k] - aj) * (t.a[k] - aj)) * t.p[k];
         s += t.p[j];
