@@ -22,9 +22,12 @@ namespace qr {
 std::atomic<int> g_demap_fast{1};
 
 template <bool FAST>
-__global__ void __launch_bounds__(256) k_demap(const DemapTables *__restrict__ tab, int B, int ld, int64_t S,
-                                               const double *__restrict__ n, const int64_t *__restrict__ j,
-                                               double alpha, double *__restrict__ lappr) {
+__global__ void __launch_bounds__(256) k_demap(const DemapTables *__restrict__ tab, const MathTables *__restrict__ gmt,
+                                               int B, int ld, int64_t S, const double *__restrict__ n,
+                                               const int64_t *__restrict__ j, double alpha,
+                                               double *__restrict__ lappr) {
+    __shared__ MathTables mt;
+    stage_math_tables(&mt, gmt);
     const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t s = item / ld;
     const int f = (int)(item - s * ld);
@@ -37,7 +40,7 @@ __global__ void __launch_bounds__(256) k_demap(const DemapTables *__restrict__ t
 #pragma unroll
         for (int k = 0; k < kMaxBps; ++k) out[k] = __builtin_nan("");
     } else {
-        demap_symbol<FAST>(t, nv, (int)jv, alpha, out);
+        demap_symbol<FAST>(t, mt, nv, (int)jv, alpha, out);
     }
     const int bps = t.bps;
 #pragma unroll
@@ -216,9 +219,9 @@ int demap_batch_device(const qr_demap *dm, int B, int ld, int64_t S, const doubl
     ProfScope ps("demap", s);
     const int64_t items = S * ld;
     if (g_demap_fast.load())
-        k_demap<true><<<(unsigned)((items + 255) / 256), 256, 0, s>>>(dm->d_tables, B, ld, S, n, j, alpha, lappr);
+        k_demap<true><<<(unsigned)((items + 255) / 256), 256, 0, s>>>(dm->d_tables, dm->d_mtab, B, ld, S, n, j, alpha, lappr);
     else
-        k_demap<false><<<(unsigned)((items + 255) / 256), 256, 0, s>>>(dm->d_tables, B, ld, S, n, j, alpha, lappr);
+        k_demap<false><<<(unsigned)((items + 255) / 256), 256, 0, s>>>(dm->d_tables, dm->d_mtab, B, ld, S, n, j, alpha, lappr);
     QR_LAUNCH_CHECK();
     return QR_OK;
 }
@@ -261,13 +264,38 @@ int qr_demap_create(int32_t bps, const double *constellation, const double *prob
     t.Fthr[M] = 1;
     for (int i = 1; i < M; ++i) t.Fthr[i] = single_F_Y(t, t.thr[i]);
     for (int i = 0; i < M; ++i) t.dF[i] = t.Fthr[i + 1] - t.Fthr[i];  // :159-162
+    t.inv_den = 1.0 / t.den;
+    t.inv_two_s2 = 1.0 / t.two_s2;
+    t.amin = t.amax = t.a[0];
+    for (int i = 1; i < M; ++i) { t.amin = fmin(t.amin, t.a[i]); t.amax = fmax(t.amax, t.a[i]); }
+    // Newton start table (qamr_math.hpp, build_quantiles): M * kQStride * M exact F_Y
+    // bisections; beyond 32-PAM its cost grows as M^2 and the brute search is used.
+    std::vector<double2> quant;
+    if (M <= 32) {
+        quant.resize((size_t)M * kQStride);
+        build_quantiles(t, quant.data());
+    }
+    std::vector<MathTables> mt(1);
+    build_math_tables(&mt[0]);
     dm->device = device;
     dm->scratch.device = device;
     DeviceGuard g(device);
-    hipError_t e = hipMalloc((void **)&dm->d_tables, sizeof(DemapTables));
+    hipError_t e = hipSuccess;
+    if (!quant.empty()) {
+        e = hipMalloc((void **)&dm->d_quant, quant.size() * sizeof(double2));
+        if (e == hipSuccess)
+            e = hipMemcpy(dm->d_quant, quant.data(), quant.size() * sizeof(double2), hipMemcpyHostToDevice);
+    }
+    t.quant = dm->d_quant;  // device pointer in the device copy
+    if (e == hipSuccess) e = hipMalloc((void **)&dm->d_mtab, sizeof(MathTables));
+    if (e == hipSuccess) e = hipMemcpy(dm->d_mtab, mt.data(), sizeof(MathTables), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc((void **)&dm->d_tables, sizeof(DemapTables));
     if (e == hipSuccess) e = hipMemcpy(dm->d_tables, &t, sizeof(DemapTables), hipMemcpyHostToDevice);
+    t.quant = nullptr;      // the host copy never dereferences it
     if (e != hipSuccess) {
-        if (dm->d_tables) (void)hipFree(dm->d_tables);
+        (void)hipFree(dm->d_tables);
+        (void)hipFree(dm->d_mtab);
+        (void)hipFree(dm->d_quant);
         delete dm;
         return hip_fail(e, "qr_demap_create upload", __FILE__, __LINE__);
     }
@@ -280,6 +308,8 @@ int qr_demap_destroy(qr_demap *dm) {
     {
         DeviceGuard g(dm->device);
         (void)hipFree(dm->d_tables);
+        (void)hipFree(dm->d_mtab);
+        (void)hipFree(dm->d_quant);
     }
     delete dm;
     return QR_OK;
@@ -321,9 +351,9 @@ int qr_demap_host(const qr_demap *dm, int64_t S, const double *n, const int64_t 
     {
         ProfScope ps("demap", nullptr);
         if (g_demap_fast.load())
-            k_demap<true><<<(unsigned)((S + 255) / 256), 256>>>(dm->d_tables, 1, 1, S, d_n, d_j, 1.0, d_l);
+            k_demap<true><<<(unsigned)((S + 255) / 256), 256>>>(dm->d_tables, dm->d_mtab, 1, 1, S, d_n, d_j, 1.0, d_l);
         else
-            k_demap<false><<<(unsigned)((S + 255) / 256), 256>>>(dm->d_tables, 1, 1, S, d_n, d_j, 1.0, d_l);
+            k_demap<false><<<(unsigned)((S + 255) / 256), 256>>>(dm->d_tables, dm->d_mtab, 1, 1, S, d_n, d_j, 1.0, d_l);
         QR_LAUNCH_CHECK();
     }
     QR_HIP(hipMemcpy(lappr, d_l, S * bps * 8, hipMemcpyDeviceToHost));

@@ -98,5 +98,7 @@ struct qr_demap {
     int device = 0;
     qr::DemapTables h;                      // host copy
     qr::DemapTables *d_tables = nullptr;    // device copy
+    qr::MathTables *d_mtab = nullptr;       // exp table for the Newton root search
+    double2 *d_quant = nullptr;             // F_Y^-1 Hermite nodes (Newton start), may be null
     mutable qr::Scratch scratch;
 };

@@ -9,6 +9,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "fastmath.hpp"
+
 #define QR_HD __host__ __device__ __forceinline__
 
 namespace qr {
@@ -112,7 +114,25 @@ struct DemapTables {
     double Fthr[kMaxOrder + 1]; // F_Y_thresholds
     double dF[kMaxOrder];       // delta_F_Y
     uint8_t sign[kMaxOrder];    // sign_config
+    double inv_den;             // 1 / den (Newton only)
+    double inv_two_s2;          // 1 / two_s2
+    double amin, amax;          // constellation extremes (Newton window bound)
+    const double2 *quant;       // [M][kQStride] F_Y^-1 Hermite nodes (Newton start), see build_quantiles
 };
+
+// Newton start table, per decision region k: nodes (y, dy/dx) of y = F_Y^-1(F_thr[k] + u dF[k])
+// for cubic Hermite interpolation in a table coordinate x (node spacing 1):
+//   left zone   u = w < 2^-kZoneOct:        x = (log2 w + kZoneDepth) * kPerOct   (kZone nodes)
+//   middle      u in [2^-kZoneOct, 1 - 2^-kZoneOct], uniform, kMid intervals      (kMid + 1 nodes)
+//   right zone  u = 1 - w, w < 2^-kZoneOct: as the left zone                     (kZone nodes)
+// The log zones straighten the tails of the outer regions and the low-density ends of
+// the inner ones; start errors stay ~1e-9 of the region width (one Newton evaluation).
+constexpr int kZoneOct = 5;
+constexpr int kZoneDepth = 56;
+constexpr int kPerOct = 16;
+constexpr int kZone = (kZoneDepth - kZoneOct) * kPerOct + 1;
+constexpr int kMid = 1024;
+constexpr int kQStride = 2 * kZone + kMid + 1;   // nodes per region (double2 each)
 
 // noisemapper.pyx:278-286 with __F_Z (:66-67): sum over m in order, m = 0 first.
 QR_HD double single_F_Y(const DemapTables& t, double y) {
@@ -146,45 +166,95 @@ QR_HD double single_F_Y(const DemapTables& t, double y) {
 // NaN instead of a stuck GPU wave.
 constexpr int kSearchCap = 2200;
 
-// Three-way comparison oracle of the search: sign(F_Y(y) - T).
+// Three-way comparison oracle of the search: sign(F_Y(y) - T).  quick() answers from
+// the certified window (2 = inside it, or no window: evaluate), exact() evaluates F_Y.
 struct SearchCmp {
     const DemapTables *t;
     double T, ystar, W;
     bool have;
-    QR_HD int operator()(double y) const {
-        if (have) {
-            const double d = y - ystar;
-            if (d > W) return 1;
-            if (d < -W) return -1;
-        }
+    QR_HD int quick(double y) const {             // selects only (no branches)
+        const double w = have ? W : __builtin_inf();
+        const double d = y - ystar;
+        const int c = (d > w) ? 1 : 2;
+        return (d < -w) ? -1 : c;
+    }
+    QR_HD int exact(double y) const {
         const double F = single_F_Y(*t, y);
         return (F > T) ? 1 : (F < T) ? -1 : 0;   // NaN -> 0 (neither > nor <)
     }
 };
 
+// The reference's bracket phase (noisemapper.pyx:314-329): up (T > .5) from [0, 1],
+// down from [-1, 0], doubling.  Straight-line body; the exact evaluation is the only
+// divergent branch.  Returns the guard count (NaN bracket past kSearchCap).
+QR_HD int search_bracket(const SearchCmp &cmp, double &lo, double &hi) {
+    const bool up = cmp.T > .5;
+    lo = up ? 0.0 : -1.0;
+    hi = up ? 1.0 : 0.0;
+    int guard = 0;
+    for (;;) {                                    // while (F_Y(hi) < T) / while (F_Y(lo) > T)
+        const double y = up ? hi : lo;
+        int c = cmp.quick(y);
+        if (c == 2) c = cmp.exact(y);
+        if (!(up ? (c < 0) : (c > 0))) break;
+        if (++guard > kSearchCap) { lo = hi = NAN; break; }
+        lo = up ? hi : 2. * lo;                   // up: lo = hi, hi *= 2; down: hi = lo, lo *= 2
+        hi = up ? 2. * hi : y;
+    }
+    return guard;
+}
+
 // The reference's bracket + bisection (noisemapper.pyx:314-345) on a comparison oracle.
 QR_HD double search_replay(const SearchCmp &cmp) {
     double lo, hi;
-    int guard = 0;
-    if (cmp.T > .5) {
-        hi = 1; lo = 0;
-        while (cmp(hi) < 0) {             // while (F_Y(hi) < T)
-            if (++guard > kSearchCap) return NAN;
-            lo = hi; hi *= 2.;
-        }
-    } else {
-        lo = -1; hi = 0;
-        while (cmp(lo) > 0) {             // while (F_Y(lo) > T)
-            if (++guard > kSearchCap) return NAN;
-            hi = lo; lo *= 2.;
-        }
-    }
+    int guard = search_bracket(cmp, lo, hi);
     while ((hi - lo) > 1e-9) {
-        if (++guard > kSearchCap) return NAN;
+        if (++guard > kSearchCap) { lo = hi = NAN; break; }
         const double mid = (hi + lo) / 2;
-        if (cmp(mid) > 0) hi = mid; else lo = mid;   // if (F_Y(mid) > T) hi = mid else lo = mid
+        int c = cmp.quick(mid);
+        if (c == 2) c = cmp.exact(mid);
+        if (c > 0) hi = mid; else lo = mid;       // if (F_Y(mid) > T) hi = mid else lo = mid
     }
     return (hi + lo) / 2;
+}
+
+// The bisection in closed form, for a certified window W < 2^-31.  The bracket width is
+// 2^e >= 1 with dyadic ends, so every mid is exact and the loop ends at width
+// g = 2^-30 (the first power of two <= 1e-9) after e + 30 halvings, on the grid
+// lo + j g.  Each mid outside the window is decided by sign(mid - ystar); the final
+// bracket [L, L + g] is the grid cell holding ystar.  Only its ends can lie within W of
+// ystar (every other mid is >= g - W away), and only an end that moved (L != lo,
+// H != hi) was a mid: at most one exact evaluation, whose answer shifts the cell by g.
+QR_HD double search_replay_closed(const SearchCmp &cmp) {
+    double lo, hi;
+    const int guard = search_bracket(cmp, lo, hi);
+    const double width = hi - lo;
+    if (!(width > 1e-9) || !(width <= 0x1p20) || !(cmp.W < 0x1p-31)) {
+        double l = lo, h = hi;                    // general loop (not reached in practice)
+        int gd = guard;
+        while ((h - l) > 1e-9) {
+            if (++gd > kSearchCap) { l = h = NAN; break; }
+            const double mid = (h + l) / 2;
+            int c = cmp.quick(mid);
+            if (c == 2) c = cmp.exact(mid);
+            if (c > 0) h = mid; else l = mid;
+        }
+        return (h + l) / 2;
+    }
+    if (guard + ilogb(width) + 30 > kSearchCap) return NAN;
+    constexpr double g = 0x1p-30;
+    double j = floor((cmp.ystar - lo) * 0x1p30);
+    j = fmin(fmax(j, 0.0), width * 0x1p30 - 1.0);
+    double L = lo + j * g;                        // exact (|L| < 2^22)
+    L = (L > cmp.ystar && L > lo) ? L - g : L;    // fix the rounding of j (exact compares)
+    L = (L + g <= cmp.ystar && L + g < hi) ? L + g : L;
+    double H = L + g;
+    if (L != lo && cmp.ystar - L <= cmp.W) {
+        if (cmp.exact(L) > 0) { H = L; L -= g; }  // F_Y(L) > T: hi = L
+    } else if (H != hi && H - cmp.ystar <= cmp.W) {
+        if (!(cmp.exact(H) > 0)) { L = H; H += g; }   // else lo = H
+    }
+    return (H + L) / 2;
 }
 
 QR_HD double search_target(const DemapTables &t, double n_hat, int i) {
@@ -198,102 +268,203 @@ QR_HD double g_inv_search(const DemapTables &t, double n_hat, int i) {
     return search_replay(cmp);
 }
 
-// F_Y(y) and its density f_Y(y) = sum_m p_m exp(-u_m^2) / (sqrt(pi) den), u_m = (y - a_m)/den.
-// Accurate to a few ulp; only steers Newton (never decides a comparison).
-QR_HD void F_and_density(const DemapTables &t, double y, double &F, double &f) {
+// exp(x) with the LDS tables of fastmath.hpp (<= ~1 ulp, like ocml/glibc exp): x = k ln2/256 + r,
+// exp(x) = 2^(k>>8) 2^((k&255)/256) e^r.  Overflows to inf above ~709.8, underflows to 0;
+// NaN propagates.
+QR_HD double exp_fast(double x, const MathTables &T) {
+    constexpr double kInvL = 0x1.71547652b82fep+8;     // 256 / ln 2
+    constexpr double kL2Hi = 0x1.62e42fefa4000p-9;
+    constexpr double kL2Lo = -0x1.8432a1b0e2634p-51;
+    const double xc = (x > 710.0) ? 710.0 : (x < -746.0) ? -746.0 : x;
+    const double kd = __builtin_rint(xc * kInvL);
+    double r = __builtin_fma(kd, -kL2Hi, xc);
+    r = __builtin_fma(kd, -kL2Lo, r);
+    const int k = (int)kd;
+    const double s = T.exp2j[k & (kExpN - 1)];
+    double p = __builtin_fma(r, 1.0 / 24.0, 1.0 / 6.0);
+    p = __builtin_fma(p, r, 0.5);
+    p = __builtin_fma(p, r * r, r);
+    return __builtin_ldexp(__builtin_fma(s, p, s), k >> kExpBits);
+}
+
+QR_HD double exp_neg_fast(double x, const MathTables &T) { return exp_fast(-x, T); }
+
+// F_Y(y), its density f_Y(y) = sum_m p_m exp(-u_m^2) / (sqrt(pi) den), u_m = (y - a_m)/den,
+// and A = max_m |u_m| (f'/f = -(2/den) * a density-weighted mean of u_m, so |f'/f| <= 2A/den).  Accurate to a
+// few ulp; only steers Newton (never decides a comparison).  Both cephes rationals are
+// evaluated branch-free and share one division.
+QR_HD void F_and_density(const DemapTables &t, const MathTables &mt, double y, double &F, double &f, double &A) {
     constexpr double kInvSqrtPi = 0.56418958354775628695;
     double sF = 0.0, sf = 0.0;
     for (int m = 0; m < t.M; ++m) {
-        const double u = (y - t.a[m]) / t.den;
+        const double u = (y - t.a[m]) * t.inv_den;
         const double au = fabs(u);
-        const double e = exp(-au * au);          // shared by the density and cephes' erfc
-        double r;
-        if (au > 1.0) {
-            double p, q;
-            if (au < 8.0) {
-                p = CephesErf::P[0];
-                for (int i = 1; i <= 8; ++i) p = p * au + CephesErf::P[i];
-                q = au + CephesErf::Q[0];
-                for (int i = 1; i < 8; ++i) q = q * au + CephesErf::Q[i];
-            } else {
-                p = CephesErf::R[0];
-                for (int i = 1; i <= 5; ++i) p = p * au + CephesErf::R[i];
-                q = au + CephesErf::S[0];
-                for (int i = 1; i < 6; ++i) q = q * au + CephesErf::S[i];
-            }
-            r = 1.0 - (e * p) / q;
-        } else {
-            const double z = au * au;
-            double p = CephesErf::T[0];
-            for (int i = 1; i <= 4; ++i) p = p * z + CephesErf::T[i];
-            double q = z + CephesErf::U[0];
-            for (int i = 1; i < 5; ++i) q = q * z + CephesErf::U[i];
-            r = au * p / q;
-        }
-        sF += (0.5 * (1 + ((u < 0.0) ? -r : r))) * t.p[m];
+        const double z = au * au;
+        const double e = exp_neg_fast(z, mt);
+        double pt = CephesErf::T[0];
+        for (int i = 1; i <= 4; ++i) pt = pt * z + CephesErf::T[i];
+        double qu = z + CephesErf::U[0];
+        for (int i = 1; i < 5; ++i) qu = qu * z + CephesErf::U[i];
+        double pp = CephesErf::P[0];
+        for (int i = 1; i <= 8; ++i) pp = pp * au + CephesErf::P[i];
+        double qq = au + CephesErf::Q[0];
+        for (int i = 1; i < 8; ++i) qq = qq * au + CephesErf::Q[i];
+        const bool small = au <= 1.0;
+        const double ratio = (small ? au * pt : e * pp) / (small ? qu : qq);   // erf (small) or erfc
+        const double er = small ? ratio : 1.0 - ratio;
+        sF += (0.5 * (1 + ((u < 0.0) ? -er : er))) * t.p[m];
         sf += e * t.p[m];
     }
     F = sF;
-    f = sf * (kInvSqrtPi / t.den);
+    f = sf * (kInvSqrtPi * t.inv_den);
+    A = fmax(fabs(y - t.amin), fabs(y - t.amax)) * t.inv_den;
 }
 
-// Safeguarded Newton for F_Y(y) = T; returns false if no certified root.
-QR_HD bool newton_root(const DemapTables &t, double T, double &ystar, double &W) {
-    if (!(T > 0.0 && T < 1.0)) return false;
-    // bracket from the decision thresholds: F_Y(t_k) = F_Y_thresholds[k]
-    int k = 0;
-    while (k < t.M && !(t.Fthr[k + 1] >= T)) ++k;
-    if (k >= t.M) return false;
-    double lo = t.thr[k], hi = t.thr[k + 1];
-    double y = (k == 0) ? t.a[0] : (k == t.M - 1) ? t.a[t.M - 1] : 0.5 * (lo + hi);
-    if (!(y > lo && y < hi)) y = 0.5 * (lo + hi);
-    double F, f, step = hi - lo;
-    bool conv = false;
-    for (int it = 0; it < 80; ++it) {
-        F_and_density(t, y, F, f);
-        const double g = F - T;
-        if (g > 0) hi = y; else lo = y;
-        double yn = y - g / f;
-        if (!(yn > lo && yn < hi)) yn = 0.5 * (lo + hi);      // bisection fallback (also f == 0 / NaN)
-        step = yn - y;
-        y = yn;
-        if (fabs(step) <= 1e-13 * (fabs(y) + t.den)) { conv = true; break; }
+// Cubic Hermite on one table interval, x in [0, 1] (node spacing 1 in the table coordinate).
+QR_HD double hermite(double2 n0, double2 n1, double x) {
+    const double x2 = x * x, x1m = x - 1.0;
+    // y0 (1 + 2x)(1-x)^2 + d0 x (1-x)^2 + y1 x^2 (3 - 2x) + d1 x^2 (x - 1)
+    return (n0.x * (1.0 + 2.0 * x) + n0.y * x) * (x1m * x1m) + (n1.x * (3.0 - 2.0 * x) + n1.y * x1m) * x2;
+}
+
+// Start point for the root of F_Y(y) = T in region k; NaN when out of the table.
+QR_HD double quantile_start(const DemapTables &t, int k, double T) {
+    const double2 *Qk = t.quant + (size_t)k * kQStride;
+    const double u = (T - t.Fthr[k]) / t.dF[k];
+    const double w = (u < 0.5) ? u : 1.0 - u;
+    if (w < 1.0 / (1 << kZoneOct)) {
+        const double x = (log2(w) + kZoneDepth) * kPerOct;
+        if (!(x >= 0.0)) return __builtin_nan("");
+        int j = (int)x;
+        if (j > kZone - 2) j = kZone - 2;
+        const double2 *Z = (u < 0.5) ? Qk : Qk + kZone + kMid + 1;
+        return hermite(Z[j], Z[j + 1], x - j);
     }
-    if (!conv) return false;
-    F_and_density(t, y, F, f);
-    if (!(f > 0.0)) return false;
-    // window: Newton residual and last step + float error of F_Y (<= (M+2) ulp(1),
-    // absolute) over the density, with a x8..x16 margin.  Any finite W is correct
-    // (ambiguous comparisons are evaluated exactly); W only sets the cost.
-    const double eps = 2.220446049250313e-16;
-    const double w = 8.0 * fabs(F - T) / f + 4.0 * fabs(step) + 16.0 * (t.M + 4) * eps / f + 8.0 * eps * fabs(y);
-    if (!(w < 1e-3)) return false;
-    ystar = y;
-    W = w;
-    return true;
+    constexpr double kLo = 1.0 / (1 << kZoneOct), kScale = kMid / (1.0 - 2.0 * kLo);
+    const double x = (u - kLo) * kScale;
+    int i = (int)x;
+    if (i < 0) i = 0;
+    if (i > kMid - 1) i = kMid - 1;
+    return hermite(Qk[kZone + i], Qk[kZone + i + 1], x - i);
+}
+
+// Newton from the Hermite start, usually one evaluation; returns false if it cannot
+// certify a window (then the brute-force search runs).  Window W bounds |ystar - y*|:
+//   Newton:  |y1 - y*| = |f'(xi)| / (2 f(y0)) (y0 - y*)^2 <= (A/den) d^2 (1 + o(1))
+//            for |d| (A + 1) <= 1e-3 den (f, A change by < 1% over the step); taken x4;
+//   float:   F_Y carries <= (M+4) eps absolute error (erf <= 4 eps, 1+erf and the
+//            product/sum roundings <= (M+1) eps), the Newton-side F_Y <= (M+6) eps, i.e.
+//            (2M+10) eps / f in y; taken x2 ((4M+20) eps / f), plus 4 eps |y|.
+// Any finite W keeps the result exact (comparisons inside W are evaluated exactly);
+// W only sets the cost.
+QR_HD bool newton_root(const DemapTables &t, const MathTables &mt, double T, int k, double &ystar, double &W) {
+    if (!t.quant || !(T > 0.0 && T < 1.0)) return false;
+    double y = quantile_start(t, k, T);
+    if (!(fabs(y) < 1e300)) return false;
+    constexpr double eps = 2.220446049250313e-16;
+    for (int it = 0; it < 4; ++it) {
+        double F, f, A;
+        F_and_density(t, mt, y, F, f, A);
+        if (!(f > 0.0)) return false;
+        const double d = (F - T) / f;
+        y -= d;
+        const double wn = 4.0 * (A + 1.0) * t.inv_den * d * d;
+        const double wf = (4.0 * t.M + 20.0) * eps / f + 4.0 * eps * fabs(y);
+        if (fabs(d) * (A + 1.0) <= 1e-3 * t.den && wn <= fmax(wf, 1e-13)) {
+            ystar = y;
+            W = wn + wf;
+            return W < 1e-3;
+        }
+    }
+    return false;
 }
 
 // Fast g_inv_search: bit-identical to g_inv_search (see the block comment).
-QR_HD double g_inv_search_fast(const DemapTables &t, double n_hat, int i) {
+QR_HD double g_inv_search_fast(const DemapTables &t, const MathTables &mt, double n_hat, int i) {
     SearchCmp cmp{&t, search_target(t, n_hat, i), 0.0, 0.0, false};
-    cmp.have = newton_root(t, cmp.T, cmp.ystar, cmp.W);
-    return search_replay(cmp);
+    cmp.have = newton_root(t, mt, cmp.T, i, cmp.ystar, cmp.W);   // T lies in region i
+    return cmp.have ? search_replay_closed(cmp) : search_replay(cmp);
+}
+
+// Host: density f_Y with libm exp (table construction only).
+inline double host_density(const DemapTables &t, double y) {
+    double s = 0.0;
+    for (int m = 0; m < t.M; ++m) {
+        const double u = (y - t.a[m]) / t.den;
+        s += t.p[m] * exp(-u * u);
+    }
+    return s * 0.56418958354775628695 / t.den;
+}
+
+// Host: F_Y^-1(P) in [lo, hi] by safeguarded Newton on the exact F_Y, from y0.
+inline double host_inverse(const DemapTables &t, double P, double lo, double hi, double y0) {
+    double y = (y0 > lo && y0 < hi) ? y0 : 0.5 * (lo + hi);
+    for (int it = 0; it < 400; ++it) {
+        const double F = single_F_Y(t, y);
+        if (F < P) lo = y; else hi = y;
+        double yn = y - (F - P) / host_density(t, y);
+        if (!(yn > lo && yn < hi)) yn = 0.5 * (lo + hi);
+        const bool done = fabs(yn - y) <= 1e-15 * fabs(y) + 1e-300 || !(hi - lo > 1e-15 * (fabs(lo) + fabs(hi)));
+        y = yn;
+        if (done) break;
+    }
+    return y;
+}
+
+// Host: the Hermite node table of quantile_start (kQStride nodes per region).
+inline void build_quantiles(const DemapTables &t, double2 *quant) {
+    constexpr double kLn2 = 0.69314718055994530942;
+    constexpr double kLo = 1.0 / (1 << kZoneOct);
+    for (int k = 0; k < t.M; ++k) {
+        double2 *Qk = quant + (size_t)k * kQStride;
+        const double L = t.thr[k], H = t.thr[k + 1];
+        auto inv = [&](double u, double lo, double hi) {
+            if (u <= 0.0) return L;
+            if (u >= 1.0) return H;
+            return host_inverse(t, t.Fthr[k] + u * t.dF[k], lo, hi, 0.5 * (lo + hi));
+        };
+        auto node = [&](double y, double dudx) {
+            double2 n;
+            n.x = y;
+            n.y = t.dF[k] / host_density(t, y) * dudx;   // dy/dx = dy/du du/dx
+            return n;
+        };
+        // middle, ascending u (each solve bracketed by the previous node)
+        double prev = L;
+        for (int i = 0; i <= kMid; ++i) {
+            const double u = kLo + (1.0 - 2.0 * kLo) * i / kMid;
+            const double y = inv(u, prev, H);
+            prev = y;
+            Qk[kZone + i] = node(y, (1.0 - 2.0 * kLo) / kMid);
+        }
+        // zones, j = 0 deepest (w = 2^-kZoneDepth) to j = kZone-1 (w = 2^-kZoneOct)
+        double plo = L, phi = H;
+        for (int j = 0; j < kZone; ++j) {
+            const double w = exp2((double)j / kPerOct - kZoneDepth);
+            const double yl = inv(w, plo, H);
+            plo = yl;
+            Qk[j] = node(yl, w * kLn2 / kPerOct);
+            const double yr = inv(1.0 - w, L, phi);
+            phi = yr;
+            Qk[kZone + kMid + 1 + j] = node(yr, -w * kLn2 / kPerOct);
+        }
+    }
 }
 
 // noisemapper.pyx:450-540 for one symbol; out[k] = LAPPR of Gray bit k (LSB first).
 // Note the reference quirk kept on purpose: no /2sigma^2 for k < j (:503-507).
 template <bool FAST = true>
-QR_HD void demap_symbol(const DemapTables& t, double n, int j, double alpha, double* out) {
+QR_HD void demap_symbol(const DemapTables& t, const MathTables& mt, double n, int j, double alpha, double* out) {
     double N[kMaxBps], D[kMaxBps];
 #pragma unroll
     for (int k = 0; k < kMaxBps; ++k) { N[k] = 0; D[k] = 0; }
     const double aj = t.a[j];
     for (int i = 0; i < t.M; ++i) {
-        const double y = FAST ? g_inv_search_fast(t, n, i) : g_inv_search(t, n, i);
+        const double y = FAST ? g_inv_search_fast(t, mt, n, i) : g_inv_search(t, n, i);
         double s = 0;
-        for (int k = 0; k < j; ++k) s += exp((2 * y - t.a[k] - aj) * (t.a[k] - aj)) * t.p[k];
+        for (int k = 0; k < j; ++k) s += exp_fast((2 * y - t.a[k] - aj) * (t.a[k] - aj), mt) * t.p[k];
         s += t.p[j];
-        for (int k = j + 1; k < t.M; ++k) s += exp((2 * y - t.a[k] - aj) * (t.a[k] - aj) / t.two_s2) * t.p[k];
+        for (int k = j + 1; k < t.M; ++k) s += exp_fast((2 * y - t.a[k] - aj) * (t.a[k] - aj) * t.inv_two_s2, mt) * t.p[k];
         const double q = t.dF[i] / s;
         int mi = i;
 #pragma unroll

@@ -17,5 +17,6 @@ STEPS=${STEPS:-tests,smoke,bench}
 [[ $STEPS == *tests* ]] && run pytest_gpu 900 python -m pytest tests -m gpu -q ${PYTEST_ARGS:--x} -p no:cacheprovider
 [[ $STEPS == *smoke* ]] && run smoke 300 python __graft_entry__.py smoke
 [[ $STEPS == *tune* ]] && run tune 900 python scripts/tune.py ${TUNE_ARGS:-}
+[[ $STEPS == *demap* ]] && run demap_bench 600 python scripts/demap_bench.py
 [[ $STEPS == *bench* ]] && run bench 900 python bench.py ${BENCH_ARGS:-}
 exit 0
