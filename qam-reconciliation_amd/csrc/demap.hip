@@ -275,6 +275,16 @@ int qr_demap_create(int32_t bps, const double *constellation, const double *prob
         quant.resize((size_t)M * kQStride);
         build_quantiles(t, quant.data());
     }
+    // Taylor table of F_Y for the Newton evaluation (qamr_math.hpp, build_ftab)
+    std::vector<double> ftab;
+    double ftab_w = 0;
+    if (!quant.empty() && build_ftab(t, ftab, t.ftab_n, t.ftab_lo, ftab_w, t.ftab_err)) {
+        t.ftab_inv_w = 1.0 / ftab_w;
+        t.ftab_h = ftab_w / 2;
+        t.ftab_inv_h = 2.0 / ftab_w;
+    } else {
+        ftab.clear();
+    }
     std::vector<MathTables> mt(1);
     build_math_tables(&mt[0]);
     dm->device = device;
@@ -286,16 +296,24 @@ int qr_demap_create(int32_t bps, const double *constellation, const double *prob
         if (e == hipSuccess)
             e = hipMemcpy(dm->d_quant, quant.data(), quant.size() * sizeof(double2), hipMemcpyHostToDevice);
     }
-    t.quant = dm->d_quant;  // device pointer in the device copy
+    if (e == hipSuccess && !ftab.empty()) {
+        e = hipMalloc((void **)&dm->d_ftab, ftab.size() * sizeof(double));
+        if (e == hipSuccess)
+            e = hipMemcpy(dm->d_ftab, ftab.data(), ftab.size() * sizeof(double), hipMemcpyHostToDevice);
+    }
+    t.quant = dm->d_quant;  // device pointers in the device copy
+    t.ftab = dm->d_ftab;
     if (e == hipSuccess) e = hipMalloc((void **)&dm->d_mtab, sizeof(MathTables));
     if (e == hipSuccess) e = hipMemcpy(dm->d_mtab, mt.data(), sizeof(MathTables), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc((void **)&dm->d_tables, sizeof(DemapTables));
     if (e == hipSuccess) e = hipMemcpy(dm->d_tables, &t, sizeof(DemapTables), hipMemcpyHostToDevice);
-    t.quant = nullptr;      // the host copy never dereferences it
+    t.quant = nullptr;      // the host copy never dereferences them
+    t.ftab = nullptr;
     if (e != hipSuccess) {
         (void)hipFree(dm->d_tables);
         (void)hipFree(dm->d_mtab);
         (void)hipFree(dm->d_quant);
+        (void)hipFree(dm->d_ftab);
         delete dm;
         return hip_fail(e, "qr_demap_create upload", __FILE__, __LINE__);
     }
@@ -310,6 +328,7 @@ int qr_demap_destroy(qr_demap *dm) {
         (void)hipFree(dm->d_tables);
         (void)hipFree(dm->d_mtab);
         (void)hipFree(dm->d_quant);
+        (void)hipFree(dm->d_ftab);
     }
     delete dm;
     return QR_OK;

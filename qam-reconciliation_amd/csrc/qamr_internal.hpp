@@ -100,5 +100,6 @@ struct qr_demap {
     qr::DemapTables *d_tables = nullptr;    // device copy
     qr::MathTables *d_mtab = nullptr;       // exp table for the Newton root search
     double2 *d_quant = nullptr;             // F_Y^-1 Hermite nodes (Newton start), may be null
+    double *d_ftab = nullptr;               // Taylor table of F_Y (Newton), may be null
     mutable qr::Scratch scratch;
 };

@@ -9,6 +9,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "fastmath.hpp"
 
 #define QR_HD __host__ __device__ __forceinline__
@@ -117,6 +119,11 @@ struct DemapTables {
     double inv_den;             // 1 / den (Newton only)
     double inv_two_s2;          // 1 / two_s2
     double amin, amax;          // constellation extremes (Newton window bound)
+    // Piecewise Taylor table of F_Y (Newton only, see build_ftab): interval j covers
+    // [lo + j w, lo + (j+1) w]; kFtabDeg+1 coefficients in t = 2 (y - lo)/w - 2j - 1.
+    const double *ftab;
+    int32_t ftab_n;
+    double ftab_lo, ftab_inv_w, ftab_h, ftab_inv_h, ftab_err;
     const double2 *quant;       // [M][kQStride] F_Y^-1 Hermite nodes (Newton start), see build_quantiles
 };
 
@@ -289,10 +296,19 @@ QR_HD double exp_fast(double x, const MathTables &T) {
 
 QR_HD double exp_neg_fast(double x, const MathTables &T) { return exp_fast(-x, T); }
 
+// True if p holds on any active lane of the wave (host: p).
+QR_HD inline bool wave_any(bool p) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __ballot(p) != 0;
+#else
+    return p;
+#endif
+}
+
 // F_Y(y), its density f_Y(y) = sum_m p_m exp(-u_m^2) / (sqrt(pi) den), u_m = (y - a_m)/den,
-// and A = max_m |u_m| (f'/f = -(2/den) * a density-weighted mean of u_m, so |f'/f| <= 2A/den).  Accurate to a
-// few ulp; only steers Newton (never decides a comparison).  Both cephes rationals are
-// evaluated branch-free and share one division.
+// and A = max_m |u_m| (f'/f = -(2/den) * a density-weighted mean of u_m, so
+// |f'/f| <= 2A/den).  Accurate to a few ulp; only steers Newton (never decides a
+// comparison).  FMA Horner; the cephes rationals share one division.
 QR_HD void F_and_density(const DemapTables &t, const MathTables &mt, double y, double &F, double &f, double &A) {
     constexpr double kInvSqrtPi = 0.56418958354775628695;
     double sF = 0.0, sf = 0.0;
@@ -301,15 +317,22 @@ QR_HD void F_and_density(const DemapTables &t, const MathTables &mt, double y, d
         const double au = fabs(u);
         const double z = au * au;
         const double e = exp_neg_fast(z, mt);
-        double pt = CephesErf::T[0];
-        for (int i = 1; i <= 4; ++i) pt = pt * z + CephesErf::T[i];
-        double qu = z + CephesErf::U[0];
-        for (int i = 1; i < 5; ++i) qu = qu * z + CephesErf::U[i];
-        double pp = CephesErf::P[0];
-        for (int i = 1; i <= 8; ++i) pp = pp * au + CephesErf::P[i];
-        double qq = au + CephesErf::Q[0];
-        for (int i = 1; i < 8; ++i) qq = qq * au + CephesErf::Q[i];
         const bool small = au <= 1.0;
+        // Only the rational(s) some lane of the wave needs (wave-uniform branches; the
+        // lanes of a wave sit in one decision region, so most components need one).
+        double pt = 1.0, qu = 1.0, pp = 1.0, qq = 1.0;
+        if (wave_any(small)) {
+            pt = CephesErf::T[0];
+            for (int i = 1; i <= 4; ++i) pt = __builtin_fma(pt, z, CephesErf::T[i]);
+            qu = z + CephesErf::U[0];
+            for (int i = 1; i < 5; ++i) qu = __builtin_fma(qu, z, CephesErf::U[i]);
+        }
+        if (wave_any(!small)) {
+            pp = CephesErf::P[0];
+            for (int i = 1; i <= 8; ++i) pp = __builtin_fma(pp, au, CephesErf::P[i]);
+            qq = au + CephesErf::Q[0];
+            for (int i = 1; i < 8; ++i) qq = __builtin_fma(qq, au, CephesErf::Q[i]);
+        }
         const double ratio = (small ? au * pt : e * pp) / (small ? qu : qq);   // erf (small) or erfc
         const double er = small ? ratio : 1.0 - ratio;
         sF += (0.5 * (1 + ((u < 0.0) ? -er : er))) * t.p[m];
@@ -318,6 +341,28 @@ QR_HD void F_and_density(const DemapTables &t, const MathTables &mt, double y, d
     F = sF;
     f = sf * (kInvSqrtPi * t.inv_den);
     A = fmax(fabs(y - t.amin), fabs(y - t.amax)) * t.inv_den;
+}
+
+// F_Y and f_Y from the Taylor table (Newton only): ~30 FMA instead of M erf.  Returns
+// false outside the table.
+constexpr int kFtabDeg = 12;
+constexpr int kFtabStride = 16;   // doubles per interval (128 B)
+QR_HD bool F_and_density_tab(const DemapTables &t, double y, double &F, double &f) {
+    const double x = (y - t.ftab_lo) * t.ftab_inv_w;
+    if (!(x >= 0.0 && x < (double)t.ftab_n)) return false;
+    const int j = (int)x;
+    // exact: h is a power of two and lo a multiple of 2h, so the centre and y - centre
+    // are exact doubles (u may leave [-1, 1] by an ulp at the interval ends)
+    const double u = (y - (t.ftab_lo + (2 * j + 1) * t.ftab_h)) * t.ftab_inv_h;
+    const double *C = t.ftab + (size_t)j * kFtabStride;
+    double F_ = C[kFtabDeg], d = kFtabDeg * C[kFtabDeg];
+    for (int k = kFtabDeg - 1; k >= 1; --k) {
+        F_ = __builtin_fma(F_, u, C[k]);
+        d = __builtin_fma(d, u, k * C[k]);
+    }
+    F = __builtin_fma(F_, u, C[0]);
+    f = d * t.ftab_inv_h;
+    return true;
 }
 
 // Cubic Hermite on one table interval, x in [0, 1] (node spacing 1 in the table coordinate).
@@ -353,8 +398,9 @@ QR_HD double quantile_start(const DemapTables &t, int k, double T) {
 //   Newton:  |y1 - y*| = |f'(xi)| / (2 f(y0)) (y0 - y*)^2 <= (A/den) d^2 (1 + o(1))
 //            for |d| (A + 1) <= 1e-3 den (f, A change by < 1% over the step); taken x4;
 //   float:   F_Y carries <= (M+4) eps absolute error (erf <= 4 eps, 1+erf and the
-//            product/sum roundings <= (M+1) eps), the Newton-side F_Y <= (M+6) eps, i.e.
-//            (2M+10) eps / f in y; taken x2 ((4M+20) eps / f), plus 4 eps |y|.
+//            product/sum roundings <= (M+1) eps), the Newton-side F_Y <= (M+6) eps
+//            (components) or ftab_err (Taylor table); their sum over f, taken x2,
+//            plus 4 eps |y|.
 // Any finite W keeps the result exact (comparisons inside W are evaluated exactly);
 // W only sets the cost.
 QR_HD bool newton_root(const DemapTables &t, const MathTables &mt, double T, int k, double &ystar, double &W) {
@@ -362,14 +408,23 @@ QR_HD bool newton_root(const DemapTables &t, const MathTables &mt, double T, int
     double y = quantile_start(t, k, T);
     if (!(fabs(y) < 1e300)) return false;
     constexpr double eps = 2.220446049250313e-16;
+    // F_Y error budget: reference F_Y (M+4) eps + this F_Y (table: ftab_err; components:
+    // (M+6) eps), taken x2
+    const double ef = 2.0 * ((t.M + 4) * eps + (t.ftab ? t.ftab_err : (t.M + 6) * eps));
     for (int it = 0; it < 4; ++it) {
-        double F, f, A;
-        F_and_density(t, mt, y, F, f, A);
+        double F, f;
+        if (t.ftab) {
+            if (!F_and_density_tab(t, y, F, f)) return false;
+        } else {
+            double A_;
+            F_and_density(t, mt, y, F, f, A_);
+        }
         if (!(f > 0.0)) return false;
         const double d = (F - T) / f;
         y -= d;
+        const double A = fmax(fabs(y - t.amin), fabs(y - t.amax)) * t.inv_den;
         const double wn = 4.0 * (A + 1.0) * t.inv_den * d * d;
-        const double wf = (4.0 * t.M + 20.0) * eps / f + 4.0 * eps * fabs(y);
+        const double wf = ef / f + 4.0 * eps * fabs(y);
         if (fabs(d) * (A + 1.0) <= 1e-3 * t.den && wn <= fmax(wf, 1e-13)) {
             ystar = y;
             W = wn + wf;
@@ -384,6 +439,68 @@ QR_HD double g_inv_search_fast(const DemapTables &t, const MathTables &mt, doubl
     SearchCmp cmp{&t, search_target(t, n_hat, i), 0.0, 0.0, false};
     cmp.have = newton_root(t, mt, cmp.T, i, cmp.ystar, cmp.W);   // T lies in region i
     return cmp.have ? search_replay_closed(cmp) : search_replay(cmp);
+}
+
+// Host: the Taylor table of F_Y (long double): interval half-width h = the power of two
+// in (sigma/16, sigma/8] over
+// [amin - 38.6 den, amax + 38.6 den] (F_Y is 0 / 1 in double beyond), coefficients
+// F^(k)(c) h^k / k! from F^(k) = sum_m p_m (-1)^(k-1) H_(k-1)(v) e^(-v^2) / (sqrt(pi) den^k),
+// v = (c - a_m)/den, H the physicists' Hermite polynomials.  The truncation error
+// (~1e-6 (h/sigma)^13 / 13! relative) is far below eps; ftab_err is the largest
+// |table - F_Y| seen on 32 points per interval (long double reference), plus the
+// Horner rounding.  Returns false (no table) when it would exceed max_n intervals.
+inline bool build_ftab(const DemapTables &t, std::vector<double> &tab, int32_t &n, double &lo, double &w,
+                       double &err, int32_t max_n = 1 << 16) {
+    const double sigma = t.den / sqrt(2.0);
+    if (!(sigma > 0 && sigma < 1e100)) return false;
+    const double h = exp2(floor(log2(sigma / 8)));
+    const double ylo = floor((t.amin - 38.6 * t.den) / (2 * h)) * (2 * h);
+    const double yhi = t.amax + 38.6 * t.den;
+    const double nn = ceil((yhi - ylo) / (2 * h));
+    if (!(nn >= 1 && nn <= max_n)) return false;
+    n = (int32_t)nn;
+    lo = ylo;
+    w = 2 * h;
+    const long double hw = h;
+    tab.assign((size_t)n * kFtabStride, 0.0);
+    const long double rsqpi = 0.564189583547756286948079451560772586L;
+    auto Fexact = [&](long double y) {
+        long double F = 0;
+        for (int m = 0; m < t.M; ++m) F += t.p[m] * 0.5L * erfcl(-(y - t.a[m]) / t.den);
+        return F;
+    };
+    for (int j = 0; j < n; ++j) {
+        const long double c = (long double)lo + (2 * j + 1) * hw;
+        long double coef[kFtabDeg + 1] = {0};
+        coef[0] = Fexact(c);
+        for (int m = 0; m < t.M; ++m) {
+            const long double v = (c - t.a[m]) / t.den;
+            const long double g = t.p[m] * expl(-v * v) * rsqpi;
+            long double Hm1 = 0, H = 1, scale = 1;               // H_0
+            for (int k = 1; k <= kFtabDeg; ++k) {
+                scale *= hw / t.den / k;                          // (h/den)^k / k!
+                coef[k] += ((k & 1) ? 1 : -1) * H * g * scale;   // (-1)^(k-1) H_(k-1)
+                const long double Hn = 2 * v * H - 2 * (k - 1) * Hm1;
+                Hm1 = H;
+                H = Hn;
+            }
+        }
+        for (int k = 0; k <= kFtabDeg; ++k) tab[(size_t)j * kFtabStride + k] = (double)coef[k];
+    }
+    // measured error (double Horner, as on the device)
+    long double e = 0;
+    for (int j = 0; j < n; ++j) {
+        const double *C = &tab[(size_t)j * kFtabStride];
+        for (int s = 0; s <= 32; ++s) {
+            const double u = -1.0 + s / 16.0;
+            double F = C[kFtabDeg];
+            for (int k = kFtabDeg - 1; k >= 0; --k) F = fma(F, u, C[k]);
+            const long double y = (long double)lo + (2 * j + 1) * hw + u * hw;
+            e = fmaxl(e, fabsl((long double)F - Fexact(y)));
+        }
+    }
+    err = (double)(2 * e) + 4 * 2.220446049250313e-16;
+    return true;
 }
 
 // Host: density f_Y with libm exp (table construction only).

@@ -42,6 +42,8 @@ int main(int argc, char** argv) {
             std::vector<double2> quant((size_t)M * qr::kQStride);
             qr::build_quantiles(t, quant.data());
             t.quant = quant.data();
+            std::vector<double> ftab; double fw = 0;
+            if (qr::build_ftab(t, ftab, t.ftab_n, t.ftab_lo, fw, t.ftab_err)) { t.ftab = ftab.data(); t.ftab_inv_w = 1 / fw; t.ftab_h = fw / 2; t.ftab_inv_h = 2 / fw; }
             for (long d = 0; d < draws / 24; ++d) {
                 double n = U(g);
                 int i = (int)(g() % M);
