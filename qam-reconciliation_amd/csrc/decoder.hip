@@ -44,6 +44,19 @@ __device__ __forceinline__ void st_msg(double *p, double v) {
     else *p = v;
 }
 
+// Row `row` (wave-uniform) of a frame-innermost array: a scalar base, so every access
+// is `global_load ... v_off, s[base]` with one 32-bit lane offset (f * 8) shared by all
+// rows instead of a 64-bit address per access (frees ~2 VGPRs per live message).
+template <typename T>
+__device__ __forceinline__ T *row_ptr(T *base, int row, int ld) {
+    return base + (size_t)(uint32_t)__builtin_amdgcn_readfirstlane(row) * (size_t)ld;
+}
+// Element at byte offset `boff` (32-bit, = f * sizeof(T)) of a wave-uniform row.
+template <typename T>
+__device__ __forceinline__ T *at_byte(T *rowp, uint32_t boff) {
+    return (T *)((char *)rowp + boff);
+}
+
 // Block geometry shared by the check and variable sweeps: 256 threads = `ft`
 // consecutive frames (ft = 64 << k, a multiple of the wavefront) x (256/ft)
 // node lanes; every wave therefore covers 64 frames of ONE node, which makes
@@ -81,9 +94,31 @@ struct VarArgs {
     unsigned nbx;
 };
 
+// The inputs of one check update: gathered posteriors, own c2v messages, syndrome bit.
+template <int D, int MODE, bool NT>
+struct CheckIn {
+    double p[D], c[D];
+    int base;
+    uint8_t sb;
+    __device__ __forceinline__ void load(const CheckArgs &a, int64_t ci, int f) {
+        const int ld = a.ld;
+        const uint32_t b8 = (uint32_t)f * 8u;
+        const int cc = a.checks[ci];
+        base = a.chk_ptr[cc];
+        sb = *at_byte(row_ptr(a.synd, cc, ld), (uint32_t)f);
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            p[i] = *at_byte(row_ptr(a.post, a.chk_var[base + i], ld), b8);
+            if (MODE == kNormal) c[i] = ld_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8));
+        }
+    }
+};
+
 // One lane = one (check, frame); each thread walks `per` checks of one degree class.
 // decoder.pyx:322-369 (F/B recursion) with the parity test of decoder.pyx:235-257
-// fused on the posteriors it gathers anyway.
+// fused on the posteriors it gathers anyway.  Software-pipelined: the gathers of
+// check j+1 are issued before the box-plus arithmetic of check j, so each wave
+// keeps its own loads in flight under its VALU work.
 template <int D, int MODE, bool NT>
 __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, unsigned by, const MathTables &tab) {
     const int ft = 1 << a.g.lft;
@@ -92,38 +127,49 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
     const int f = a.f_off + (int)(by << a.g.lft) + (threadIdx.x & (ft - 1));
     const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> a.g.lft);
     if (!a.active[f]) return;
-    const int64_t c0 = (int64_t)bx * a.g.per * nsub + sub;
+    int64_t ci = (int64_t)bx * a.g.per * nsub + sub;
+    if (ci >= a.n_checks) return;
     uint32_t bad = 0;
+    CheckIn<D, MODE, NT> nx;
+    nx.load(a, ci, f);
     for (int j = 0; j < a.g.per; ++j) {
-        const int64_t ci = c0 + (int64_t)j * nsub;
-        if (ci >= a.n_checks) break;
-        const int c = a.checks[ci];
-        const int base = a.chk_ptr[c];
-        const uint8_t sb = a.synd[(size_t)c * ld + f];
-        uint32_t par = sb;
+        // consume check j's inputs (m, parity) before its registers take check j+1's
+        uint32_t par = nx.sb;
         double m[D];
 #pragma unroll
         for (int i = 0; i < D; ++i) {
-            const double p = a.post[(size_t)a.chk_var[base + i] * ld + f];
+            const double p = nx.p[i];
             if (MODE != kFirst) par ^= (p < 0.0) ? 1u : 0u;   // decoder.pyx:243-246
-            if (MODE == kNormal) m[i] = p - ld_msg<NT>(&a.c2v[(size_t)a.chk_edge[base + i] * ld + f]);  // :296-297
+            if (MODE == kNormal) m[i] = p - nx.c[i];           // :296-297
             else m[i] = p;  // first sweep: c2v == 0 and p - 0.0 == p
         }
+        struct { int base; uint8_t sb; } cur = {nx.base, nx.sb};
+        const int64_t cn = ci + nsub;
+        const bool more = (j + 1 < a.g.per) && cn < a.n_checks;   // wave-uniform
+        if (more) nx.load(a, cn, f);
         if (MODE != kFirst) bad |= (par == 1u) ? 1u : 0u;  // satisfied iff (parity ^ 1) != 0
-        if (MODE == kParityOnly) continue;
-        double F[D], Bk[D];
-        F[0] = m[0];
+        if (MODE != kParityOnly) {
+            // F[i] = bp(F[i-1], m[i]); the backward values B[i] = bp(B[i+1], m[i]) are
+            // consumed as they are produced (out_i = bp(F[i-1], B[i+1])): the same
+            // operands as decoder.pyx:341-367, one live B instead of D.
+            const int base = cur.base;
+            const uint32_t b8 = (uint32_t)f * 8u;
+            const double s = cur.sb ? -1.0 : 1.0;
+            double F[D - 1];
+            F[0] = m[0];
 #pragma unroll
-        for (int i = 1; i < D - 1; ++i) F[i] = box_plus_fast(F[i - 1], m[i], tab);
-        Bk[D - 1] = m[D - 1];
+            for (int i = 1; i < D - 1; ++i) F[i] = box_plus_fast(F[i - 1], m[i], tab);
+            st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + D - 1], ld), b8), s * F[D - 2]);
+            double Bn = m[D - 1];
 #pragma unroll
-        for (int i = D - 2; i > 0; --i) Bk[i] = box_plus_fast(Bk[i + 1], m[i], tab);
-        const double s = sb ? -1.0 : 1.0;
-        st_msg<NT>(&a.c2v[(size_t)a.chk_edge[base] * ld + f], s * Bk[1]);
-#pragma unroll
-        for (int i = 1; i < D - 1; ++i)
-            st_msg<NT>(&a.c2v[(size_t)a.chk_edge[base + i] * ld + f], s * box_plus_fast(F[i - 1], Bk[i + 1], tab));
-        st_msg<NT>(&a.c2v[(size_t)a.chk_edge[base + D - 1] * ld + f], s * F[D - 2]);
+            for (int i = D - 2; i > 0; --i) {
+                st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), s * box_plus_fast(F[i - 1], Bn, tab));
+                Bn = box_plus_fast(Bn, m[i], tab);
+            }
+            st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base], ld), b8), s * Bn);
+        }
+        if (!more) break;
+        ci = cn;
     }
     if (MODE != kFirst && bad) a.unsat[f] = 1;  // benign race: every writer stores 1
 }
@@ -174,8 +220,15 @@ __global__ void __launch_bounds__(256) k_var(VarArgs a) {
 // spread over the 1-D grid, in proportion to their counts) lets the dispatcher
 // co-schedule them on every CU, so the message stream of one hides under the
 // transcendental arithmetic of the other.
+// Occupancy floor of the fused sweep: 6 waves/SIMD (80 VGPRs, a few spilled bytes)
+// beats the 4 waves the software-pipelined check sweep would get unconstrained
+// (3.27 vs 3.43 ms per launch on MI355X; scripts/exp_build.sh QR_FUSED_WAVES=n).
+#ifndef QR_FUSED_WAVES
+#define QR_FUSED_WAVES 6
+#endif
+#define QR_FUSED_ATTR __attribute__((amdgpu_waves_per_eu(QR_FUSED_WAVES, 8)))
 template <int D, int MODE, bool NT>
-__global__ void __launch_bounds__(256) k_fused(CheckArgs ca, VarArgs va, unsigned nb_check, unsigned nb_total) {
+__global__ void __launch_bounds__(256) QR_FUSED_ATTR k_fused(CheckArgs ca, VarArgs va, unsigned nb_check, unsigned nb_total) {
     __shared__ MathTables tab;
     const unsigned b = blockIdx.x;
     const unsigned c0 = (unsigned)(((uint64_t)b * nb_check) / nb_total);
@@ -292,7 +345,7 @@ static DecodeWs carve(const qr_code *code, int ld, void *base) {
 
 // Runtime tuning knobs (qr_tune_set); defaults picked by scripts/tune.py on MI355X.
 struct Tuning {
-    std::atomic<int> check_ft{256}, check_per{4}, var_ft{256}, var_per{4}, nt{1}, split{2};
+    std::atomic<int> check_ft{256}, check_per{8}, var_ft{256}, var_per{8}, nt{1}, split{2};
 };
 static Tuning g_tune;
 

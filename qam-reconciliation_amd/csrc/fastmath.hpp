@@ -9,7 +9,7 @@
 // same expression in ~22 fp64 + ~8 integer VALU operations, specialised to its
 // domain t >= 0:
 //
-//   * t > 37.5 is clamped to 37.5: there exp(-t) < 2^-54, fl(1 + exp(-t)) == 1
+//   * t > 37.5 is clamped to [37.5, 37.5 + 2^-15): there exp(-t) < 2^-54, fl(1 + exp(-t)) == 1
 //     and log(1) == 0 exactly, which is what the reference returns for every
 //     t >= 36.74 -- so the clamp changes nothing and needs no branch.  NaN
 //     survives the clamp and propagates (1 + exp(NaN) -> log(NaN) in the reference).
@@ -21,7 +21,7 @@
 //     bits of u (i = 512 for u = 2): u needs no exponent split because u <= 2.
 //     Interval 0 is centred on 1 (invc_0 = 1, logc_0 = 0) so q = u - 1 exactly and
 //     h keeps full relative accuracy as u -> 1; |q| <= 2^-9 (i = 0), 2^-10
-//     otherwise; log1p to degree 7.
+//     otherwise; log1p to degree 6.
 //   * sgn(a)sgn(b)min(|a|,|b|) == copysign(min(|a|,|b|), a*b) up to the sign of
 //     an exact zero and to NaN cases, neither of which can change bp's final value
 //     (a NaN operand makes h(|a+-b|) NaN; a zero m adds a zero to h >= 0).
@@ -79,7 +79,11 @@ __host__ __device__ __forceinline__ double h_softplus_neg(double t, const MathTa
     constexpr double kInvL = 0x1.71547652b82fep+8;     // 256 / ln 2
     constexpr double kL2Hi = 0x1.62e42fefa4000p-9;     // ln2/256, 40 significant bits
     constexpr double kL2Lo = -0x1.8432a1b0e2634p-51;   // ln2/256 - kL2Hi
-    const double tc = (t > 37.5) ? 37.5 : t;           // NaN passes through
+    // clamp t > 37.5 into [37.5, 37.5 + 2^-15) by replacing the high word only (one
+    // select instead of two; h == 0 there exactly); NaN fails the compare and passes.
+    const uint64_t tb = __builtin_bit_cast(uint64_t, t);
+    const uint32_t thi = (t > 37.5) ? 0x4042C000u : (uint32_t)(tb >> 32);
+    const double tc = __builtin_bit_cast(double, ((uint64_t)thi << 32) | (uint32_t)tb);
     const double kd = __builtin_rint(tc * -kInvL);
     double r = __builtin_fma(kd, -kL2Hi, -tc);
     r = __builtin_fma(kd, -kL2Lo, r);
@@ -95,9 +99,9 @@ __host__ __device__ __forceinline__ double h_softplus_neg(double t, const MathTa
     i = (i < (uint32_t)kLogN) ? i : (uint32_t)kLogN;    // in range for NaN too
     const double2 c = T.logt[i];
     const double q = __builtin_fma(u, c.x, -1.0);
-    // log1p(q) = q + q^2 (-1/2 + q/3 - q^2/4 + q^3/5 - q^4/6 + q^5/7)
-    double w = __builtin_fma(q, 1.0 / 7.0, -1.0 / 6.0);
-    w = __builtin_fma(w, q, 1.0 / 5.0);
+    // log1p(q) = q + q^2 (-1/2 + q/3 - q^2/4 + q^3/5 - q^4/6): |q| < 2^-9, the
+    // truncation q^7/7 < 2^-65 is far below the rounding of 1 + e
+    double w = __builtin_fma(q, -1.0 / 6.0, 1.0 / 5.0);
     w = __builtin_fma(w, q, -1.0 / 4.0);
     w = __builtin_fma(w, q, 1.0 / 3.0);
     w = __builtin_fma(w, q, -0.5);
@@ -109,7 +113,12 @@ __host__ __device__ __forceinline__ double h_softplus_neg(double t, const MathTa
 __host__ __device__ __forceinline__ double box_plus_fast(double a, double b, const MathTables &T) {
     const double m = fmin(fabs(a), fabs(b));
     const double sm = copysign(m, a * b);
+#ifdef QR_EXPERIMENT_MINSUM   // roofline experiments only (scripts/exp_build.sh): no transcendentals
+    (void)T;
+    return sm;
+#else
     return (sm + h_softplus_neg(fabs(a + b), T)) - h_softplus_neg(fabs(a - b), T);
+#endif
 }
 
 }  // namespace qr

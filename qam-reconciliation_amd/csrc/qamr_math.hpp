@@ -297,7 +297,7 @@ QR_HD double exp_fast(double x, const MathTables &T) {
 QR_HD double exp_neg_fast(double x, const MathTables &T) { return exp_fast(-x, T); }
 
 // True if p holds on any active lane of the wave (host: p).
-QR_HD inline bool wave_any(bool p) {
+QR_HD bool wave_any(bool p) {
 #ifdef __HIP_DEVICE_COMPILE__
     return __ballot(p) != 0;
 #else

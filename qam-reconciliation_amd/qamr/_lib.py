@@ -13,7 +13,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libqamr.so")
+# QAMR_LIB overrides the library path (experiment builds, scripts/exp_build.sh).
+LIB_PATH = os.environ.get("QAMR_LIB") or os.path.join(_HERE, "libqamr.so")
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 
 QR_OK, QR_EVALUE, QR_EMEMORY, QR_EDEVICE, QR_EUNSUPPORTED = 0, 1, 2, 3, 4
