@@ -128,3 +128,38 @@ def test_syndrome_and_counters_vs_oracle(gpu):
     c = pipe.counters.cpu().numpy()
     assert c[0] == errs.sum() and c[1] == (errs > 0).sum() and c[2] == s2.sum()
     assert c[3] == i2[s2 == 1].sum() and c[4] == 130
+
+
+@pytest.mark.parametrize("bps,snr", [(1, 0.0), (2, 3.0), (2, 25.0), (3, 9.5), (4, 13.0), (4, 25.0), (4, 40.0)])
+def test_fast_root_search_bit_identical_to_brute_force(gpu, bps, snr):
+    """The Newton-located, replayed root search (default) returns the same doubles as
+    the reference's brute-force bracket + bisection (qr_tune demap_fast=0) on every
+    symbol: uniform n_hat, the edge values 0 / 1 / tiny, both sign configurations."""
+    import torch
+    from qamr import _lib
+
+    pa = __import__("qamr").PAMAlphabet(bps, 2.0)
+    nv = pa.variance * 10 ** (-snr / 10) / 2
+    M = 1 << bps
+    cfg = np.array([i & 1 for i in range(M)], np.uint8)
+    nm = _nm(bps, nv, cfg)
+    rng = np.random.default_rng(bps * 100 + int(snr))
+    S, ld = 2000, 64
+    n = rng.random((S, ld))
+    n[0, :6] = [0.0, 1.0, 1e-300, 1e-17, 1 - 1e-16, 0.5]
+    n[1:4] = rng.random((3, ld)) * 1e-12
+    x = rng.integers(0, M, (S, ld))
+    dev = torch.device("cuda", 0)
+    nt = torch.from_numpy(n).to(dev).contiguous()
+    xt = torch.from_numpy(x).to(dev).contiguous()
+    try:
+        _lib.tune_set("demap_fast", 1)
+        fast = nm.demap_device(nt, xt, ld).clone()
+        _lib.tune_set("demap_fast", 0)
+        brute = nm.demap_device(nt, xt, ld).clone()
+    finally:
+        _lib.tune_set("demap_fast", 1)
+    torch.cuda.synchronize()
+    a, b = fast.cpu().numpy(), brute.cpu().numpy()
+    same = (a.view(np.int64) == b.view(np.int64)) | (np.isnan(a) & np.isnan(b))
+    assert same.all(), f"{(~same).sum()} LAPPRs differ"
