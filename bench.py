@@ -59,13 +59,32 @@ def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal knobs (several ranks on a 1-GPU box): QAMR_BENCH_DEVICE pins every
+    # rank to one device, QAMR_BENCH_BACKEND=gloo replaces RCCL (which refuses two
+    # ranks on one GPU).  The driver's N-GPU runs use neither.
+    local = int(os.environ.get("QAMR_BENCH_DEVICE", local))
     if world > 1:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if os.environ.get("QAMR_BENCH_BACKEND", "nccl") == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, local
+
+
+def reduce_(t, op):
+    """All-reduce a small GPU tensor (via the host under gloo)."""
+    import torch.distributed as dist
+
+    if dist.get_backend() == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, op=op)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op)
 
 
 def var_sweep_bytes(V, E, B):
@@ -197,8 +216,8 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        dist.all_reduce(counters, op=dist.ReduceOp.SUM)
+        reduce_(t_max, dist.ReduceOp.MAX)
+        reduce_(counters, dist.ReduceOp.SUM)
     elapsed = float(t_max.item())
     total_frames = world * batch.B * args.steps
     value = total_frames / elapsed
