@@ -21,8 +21,11 @@ namespace qr {
 // 1 = Newton-located root + replayed bisection (bit-identical, ~5x fewer erf), 0 = brute force.
 std::atomic<int> g_demap_fast{1};
 
-template <bool FAST>
-__global__ void __launch_bounds__(256) k_demap(const DemapTables *__restrict__ tab, const MathTables *__restrict__ gmt,
+#ifndef QR_DEMAP_WAVES
+#define QR_DEMAP_WAVES 4   // 4 waves/SIMD: 14.2 vs 15.8 ms (4-PAM), 52.9 vs 56.6 ms (16-PAM) per 4096 frames
+#endif
+template <bool FAST, int BPS>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QR_DEMAP_WAVES, 8))) k_demap(const DemapTables *__restrict__ tab, const MathTables *__restrict__ gmt,
                                                int B, int ld, int64_t S, const double *__restrict__ n,
                                                const int64_t *__restrict__ j, double alpha,
                                                double *__restrict__ lappr) {
@@ -35,17 +38,36 @@ __global__ void __launch_bounds__(256) k_demap(const DemapTables *__restrict__ t
     const DemapTables &t = *tab;
     const double nv = n[s * ld + f];
     const int64_t jv = j[s * ld + f];
-    double out[kMaxBps];
-    if (jv < 0 || jv >= t.M) {
+    double out[BPS];
+    if (jv < 0 || jv >= (1 << BPS)) {
 #pragma unroll
-        for (int k = 0; k < kMaxBps; ++k) out[k] = __builtin_nan("");
+        for (int k = 0; k < BPS; ++k) out[k] = __builtin_nan("");
     } else {
-        demap_symbol<FAST>(t, mt, nv, (int)jv, alpha, out);
+        demap_symbol<FAST, BPS>(t, mt, nv, (int)jv, alpha, out);
     }
-    const int bps = t.bps;
 #pragma unroll
-    for (int k = 0; k < kMaxBps; ++k)
-        if (k < bps) lappr[(s * bps + k) * ld + f] = out[k];
+    for (int k = 0; k < BPS; ++k) lappr[(s * BPS + k) * ld + f] = out[k];
+}
+
+template <int BPS>
+static void launch_demap(bool fast, unsigned grid, hipStream_t st, const qr_demap *dm, int B, int ld, int64_t S,
+                         const double *n, const int64_t *j, double alpha, double *lappr) {
+    if (fast) k_demap<true, BPS><<<grid, 256, 0, st>>>(dm->d_tables, dm->d_mtab, B, ld, S, n, j, alpha, lappr);
+    else k_demap<false, BPS><<<grid, 256, 0, st>>>(dm->d_tables, dm->d_mtab, B, ld, S, n, j, alpha, lappr);
+}
+
+static void launch_demap_bps(int bps, bool fast, unsigned grid, hipStream_t st, const qr_demap *dm, int B, int ld,
+                             int64_t S, const double *n, const int64_t *j, double alpha, double *lappr) {
+    switch (bps) {
+        case 1: launch_demap<1>(fast, grid, st, dm, B, ld, S, n, j, alpha, lappr); break;
+        case 2: launch_demap<2>(fast, grid, st, dm, B, ld, S, n, j, alpha, lappr); break;
+        case 3: launch_demap<3>(fast, grid, st, dm, B, ld, S, n, j, alpha, lappr); break;
+        case 4: launch_demap<4>(fast, grid, st, dm, B, ld, S, n, j, alpha, lappr); break;
+        case 5: launch_demap<5>(fast, grid, st, dm, B, ld, S, n, j, alpha, lappr); break;
+        case 6: launch_demap<6>(fast, grid, st, dm, B, ld, S, n, j, alpha, lappr); break;
+        case 7: launch_demap<7>(fast, grid, st, dm, B, ld, S, n, j, alpha, lappr); break;
+        default: launch_demap<8>(fast, grid, st, dm, B, ld, S, n, j, alpha, lappr); break;
+    }
 }
 
 // Bob: hard decision (noisemapper.pyx:349-359), transformed noise g(y, x_hat)
@@ -218,10 +240,8 @@ int demap_batch_device(const qr_demap *dm, int B, int ld, int64_t S, const doubl
     DeviceGuard g(dm->device);
     ProfScope ps("demap", s);
     const int64_t items = S * ld;
-    if (g_demap_fast.load())
-        k_demap<true><<<(unsigned)((items + 255) / 256), 256, 0, s>>>(dm->d_tables, dm->d_mtab, B, ld, S, n, j, alpha, lappr);
-    else
-        k_demap<false><<<(unsigned)((items + 255) / 256), 256, 0, s>>>(dm->d_tables, dm->d_mtab, B, ld, S, n, j, alpha, lappr);
+    launch_demap_bps(dm->h.bps, g_demap_fast.load() != 0, (unsigned)((items + 255) / 256), s, dm, B, ld, S, n, j,
+                     alpha, lappr);
     QR_LAUNCH_CHECK();
     return QR_OK;
 }
@@ -369,10 +389,8 @@ int qr_demap_host(const qr_demap *dm, int64_t S, const double *n, const int64_t 
     // ld = 1, B = 1: item = s, f = 0; lappr index (s*bps + k) * 1 + 0 = interleaved output.
     {
         ProfScope ps("demap", nullptr);
-        if (g_demap_fast.load())
-            k_demap<true><<<(unsigned)((S + 255) / 256), 256>>>(dm->d_tables, dm->d_mtab, 1, 1, S, d_n, d_j, 1.0, d_l);
-        else
-            k_demap<false><<<(unsigned)((S + 255) / 256), 256>>>(dm->d_tables, dm->d_mtab, 1, 1, S, d_n, d_j, 1.0, d_l);
+        launch_demap_bps(dm->h.bps, g_demap_fast.load() != 0, (unsigned)((S + 255) / 256), nullptr, dm, 1, 1, S, d_n,
+                         d_j, 1.0, d_l);
         QR_LAUNCH_CHECK();
     }
     QR_HIP(hipMemcpy(lappr, d_l, S * bps * 8, hipMemcpyDeviceToHost));

@@ -570,33 +570,34 @@ inline void build_quantiles(const DemapTables &t, double2 *quant) {
 
 // noisemapper.pyx:450-540 for one symbol; out[k] = LAPPR of Gray bit k (LSB first).
 // Note the reference quirk kept on purpose: no /2sigma^2 for k < j (:503-507).
-template <bool FAST = true>
+// BPS (= t.bps) is a template parameter: exact-size accumulators (fewer VGPRs, higher
+// occupancy) and compile-time trip counts for the M = 2^BPS hypothesis / LLR loops.
+template <bool FAST, int BPS>
 QR_HD void demap_symbol(const DemapTables& t, const MathTables& mt, double n, int j, double alpha, double* out) {
-    double N[kMaxBps], D[kMaxBps];
+    constexpr int M = 1 << BPS;
+    double N[BPS], D[BPS];
 #pragma unroll
-    for (int k = 0; k < kMaxBps; ++k) { N[k] = 0; D[k] = 0; }
+    for (int k = 0; k < BPS; ++k) { N[k] = 0; D[k] = 0; }
     const double aj = t.a[j];
-    for (int i = 0; i < t.M; ++i) {
+#pragma unroll 1
+    for (int i = 0; i < M; ++i) {
         const double y = FAST ? g_inv_search_fast(t, mt, n, i) : g_inv_search(t, n, i);
         double s = 0;
         for (int k = 0; k < j; ++k) s += exp_fast((2 * y - t.a[k] - aj) * (t.a[k] - aj), mt) * t.p[k];
         s += t.p[j];
-        for (int k = j + 1; k < t.M; ++k) s += exp_fast((2 * y - t.a[k] - aj) * (t.a[k] - aj) * t.inv_two_s2, mt) * t.p[k];
+        for (int k = j + 1; k < M; ++k) s += exp_fast((2 * y - t.a[k] - aj) * (t.a[k] - aj) * t.inv_two_s2, mt) * t.p[k];
         const double q = t.dF[i] / s;
         int mi = i;
 #pragma unroll
-        for (int k = 0; k < kMaxBps; ++k) {
-            if (k < t.bps) {
-                if ((mi * (mi + 1)) & 3) D[k] += q;
-                else                     N[k] += q;
-                mi >>= 1;
-            }
+        for (int k = 0; k < BPS; ++k) {
+            if ((mi * (mi + 1)) & 3) D[k] += q;
+            else                     N[k] += q;
+            mi >>= 1;
         }
     }
     // reconciliation.pyx:144-145 (lappr *= alpha) fused into the store.
 #pragma unroll
-    for (int k = 0; k < kMaxBps; ++k)
-        if (k < t.bps) out[k] = (log(N[k]) - log(D[k])) * alpha;
+    for (int k = 0; k < BPS; ++k) out[k] = (log(N[k]) - log(D[k])) * alpha;
 }
 
 // noisemapper.pyx:27-44 (__binsearch over the M+1 thresholds), iterative.
