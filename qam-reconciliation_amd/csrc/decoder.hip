@@ -95,6 +95,12 @@ struct VarArgs {
 };
 
 // The inputs of one check update: gathered posteriors, own c2v messages, syndrome bit.
+// Prefetch depth: the gathered posteriors of check j+1 are always issued before the
+// arithmetic of check j; its own (streamed, row-contiguous) messages are loaded on
+// use unless QR_PREFETCH_C=1 -- 14 fewer live VGPRs, 3.19 vs 3.25 ms per launch.
+#ifndef QR_PREFETCH_C
+#define QR_PREFETCH_C 0
+#endif
 template <int D, int MODE, bool NT>
 struct CheckIn {
     double p[D], c[D];
@@ -109,16 +115,22 @@ struct CheckIn {
 #pragma unroll
         for (int i = 0; i < D; ++i) {
             p[i] = *at_byte(row_ptr(a.post, a.chk_var[base + i], ld), b8);
-            if (MODE == kNormal) c[i] = ld_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8));
+            if (MODE == kNormal && QR_PREFETCH_C) c[i] = ld_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8));
         }
+    }
+    __device__ __forceinline__ void load_c(const CheckArgs &a, int f) {
+        if (MODE != kNormal || QR_PREFETCH_C) return;
+        const uint32_t b8 = (uint32_t)f * 8u;
+#pragma unroll
+        for (int i = 0; i < D; ++i) c[i] = ld_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], a.ld), b8));
     }
 };
 
 // One lane = one (check, frame); each thread walks `per` checks of one degree class.
 // decoder.pyx:322-369 (F/B recursion) with the parity test of decoder.pyx:235-257
-// fused on the posteriors it gathers anyway.  Software-pipelined: the gathers of
-// check j+1 are issued before the box-plus arithmetic of check j, so each wave
-// keeps its own loads in flight under its VALU work.
+// fused on the posteriors it gathers anyway.  Software-pipelined: the posterior
+// gathers of check j+1 are issued before the box-plus arithmetic of check j, so
+// each wave keeps its own loads in flight under its VALU work.
 template <int D, int MODE, bool NT>
 __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, unsigned by, const MathTables &tab) {
     const int ft = 1 << a.g.lft;
@@ -134,6 +146,7 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
     nx.load(a, ci, f);
     for (int j = 0; j < a.g.per; ++j) {
         // consume check j's inputs (m, parity) before its registers take check j+1's
+        nx.load_c(a, f);
         uint32_t par = nx.sb;
         double m[D];
 #pragma unroll
@@ -222,7 +235,8 @@ __global__ void __launch_bounds__(256) k_var(VarArgs a) {
 // transcendental arithmetic of the other.
 // Occupancy floor of the fused sweep: 6 waves/SIMD (80 VGPRs, a few spilled bytes)
 // beats the 4 waves the software-pipelined check sweep would get unconstrained
-// (3.27 vs 3.43 ms per launch on MI355X; scripts/exp_build.sh QR_FUSED_WAVES=n).
+// (3.19 vs 3.28 (5 waves) / 3.23 (7 waves) ms per launch on MI355X;
+// scripts/exp_build.sh QR_FUSED_WAVES=n).
 #ifndef QR_FUSED_WAVES
 #define QR_FUSED_WAVES 6
 #endif
