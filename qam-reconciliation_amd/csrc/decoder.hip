@@ -359,7 +359,7 @@ static DecodeWs carve(const qr_code *code, int ld, void *base) {
 
 // Runtime tuning knobs (qr_tune_set); defaults picked by scripts/tune.py on MI355X.
 struct Tuning {
-    std::atomic<int> check_ft{256}, check_per{8}, var_ft{256}, var_per{8}, nt{1}, split{2};
+    std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{2};
 };
 static Tuning g_tune;
 
