@@ -581,11 +581,21 @@ QR_HD void demap_symbol(const DemapTables& t, const MathTables& mt, double n, in
     const double aj = t.a[j];
 #pragma unroll 1
     for (int i = 0; i < M; ++i) {
+#ifdef QR_EXPERIMENT_NO_SEARCH   // cost-breakdown experiments only (scripts/exp_build.sh)
+        const double y = quantile_start(t, i, search_target(t, n, i));
+#else
         const double y = FAST ? g_inv_search_fast(t, mt, n, i) : g_inv_search(t, n, i);
+#endif
         double s = 0;
+#ifndef QR_EXPERIMENT_NO_LLR
         for (int k = 0; k < j; ++k) s += exp_fast((2 * y - t.a[k] - aj) * (t.a[k] - aj), mt) * t.p[k];
+#endif
         s += t.p[j];
+#ifndef QR_EXPERIMENT_NO_LLR
         for (int k = j + 1; k < M; ++k) s += exp_fast((2 * y - t.a[k] - aj) * (t.a[k] - aj) * t.inv_two_s2, mt) * t.p[k];
+#else
+        s += y * 1e-300;
+#endif
         const double q = t.dF[i] / s;
         int mi = i;
 #pragma unroll
