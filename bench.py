@@ -150,6 +150,36 @@ def cpu_baseline(args, vid, cid, pipe, batch, lappr_host_fn, budget_s):
                       f"oracle/qamr_oracle.c (gcc -O2 -ffp-contract=off, OpenMP over frames) on {cpu_model}"}
 
 
+def copy_bandwidth(dev, nbytes=2 << 30, reps=5):
+    """Measured device-to-device streaming copy bandwidth (read + write bytes / time,
+    libqamr's 16-B-per-lane copy kernel): the practical HBM ceiling SURVEY.md 8(d)
+    asks the roofline to be related to."""
+    import ctypes
+    import torch
+    from qamr import _lib
+
+    a = torch.ones(nbytes // 8, dtype=torch.float64, device=dev)
+    b = torch.empty_like(a)
+    st = torch.cuda.current_stream(dev)
+    L = _lib.load()
+
+    def cp():
+        _lib.check(L.qr_stream_copy(ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()), nbytes,
+                                    ctypes.c_void_p(st.cuda_stream)))
+    cp()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        cp()
+    e1.record(st)
+    torch.cuda.synchronize(dev)
+    gbps = 2 * nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return gbps
+
+
 def main():
     args = parse()
     import torch
@@ -259,10 +289,13 @@ def main():
                         traffic = t.get("hbm_bytes_per_launch")
                 except Exception:
                     traffic = None
+            copy_gbps = copy_bandwidth(dev) if rank == 0 else None
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
                     "bytes_per_launch": int(bytes_launch), "avg_launch_us": round(avg_s * 1e6, 1),
-                    "launches": kstats[kkey]["launches"]}
+                    "launches": kstats[kkey]["launches"],
+                    "measured_copy_GBps": round(copy_gbps, 1) if copy_gbps else None,
+                    "frac_of_copy": round(ach / copy_gbps, 4) if copy_gbps else None}
     # whole-decode algorithmic bandwidth (SURVEY.md 8(d) B_frame at the iterations actually run)
     it_mean = float(its.float().mean().item())
     V, C, E = dec.vnum, dec.cnum, dec.ednum

@@ -177,6 +177,15 @@ int launch_transpose_to_fi_i64(int B, int ld, int64_t n, const int64_t *src, int
 }  // namespace qr
 
 // ===================================================================== C-ABI
+namespace qr {
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) k_stream_copy(const u32x4 *__restrict__ src, u32x4 *__restrict__ dst, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(&src[i]), &dst[i]);
+}
+}  // namespace qr
+
 extern "C" {
 
 const char *qr_last_error(void) { return qr::g_err.c_str(); }
@@ -227,6 +236,17 @@ int qr_to_frame_innermost_u8(int32_t B, int32_t ld, int64_t n, const uint8_t *s,
 }
 int qr_to_frame_innermost_i64(int32_t B, int32_t ld, int64_t n, const int64_t *s, int64_t *d, void *st) {
     return qr::launch_transpose_to_fi_i64(B, ld, n, s, d, (hipStream_t)st);
+}
+
+int qr_stream_copy(const void *src, void *dst, int64_t bytes, void *st) {
+    if (!src || !dst || bytes < 0 || (bytes & 15) || (((uintptr_t)src | (uintptr_t)dst) & 15))
+        return qr::set_error(QR_EVALUE, "qr_stream_copy: 16-B aligned pointers and a multiple of 16 bytes required");
+    if (bytes == 0) return QR_OK;
+    const int64_t n = bytes / 16;
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 256 * 64);
+    qr::k_stream_copy<<<grid, 256, 0, (hipStream_t)st>>>((const qr::u32x4 *)src, (qr::u32x4 *)dst, n);
+    QR_LAUNCH_CHECK();
+    return QR_OK;
 }
 
 }  // extern "C"
