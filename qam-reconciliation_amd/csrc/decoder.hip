@@ -138,7 +138,11 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
     const int ld = a.ld;
     const int f = a.f_off + (int)(by << a.g.lft) + (threadIdx.x & (ft - 1));
     const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> a.g.lft);
-    if (!a.active[f]) return;
+    // Waves whose 64 frames all stopped leave; in a partly stopped wave the stopped
+    // lanes run along (no divergent exit, so the loop state stays scalar): their
+    // messages are never read again and their posteriors (the output) are not touched.
+    const bool act = a.active[f] != 0;
+    if (!wave_any(act)) return;
     int64_t ci = (int64_t)bx * a.g.per * nsub + sub;
     if (ci >= a.n_checks) return;
     uint32_t bad = 0;
@@ -184,7 +188,7 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
         if (!more) break;
         ci = cn;
     }
-    if (MODE != kFirst && bad) a.unsat[f] = 1;  // benign race: every writer stores 1
+    if (MODE != kFirst && bad && act) a.unsat[f] = 1;  // benign race: every writer stores 1
 }
 
 // decoder.pyx:285-298: post[v] = lappr[v] + c2v[e_0] + c2v[e_1] + ... (ascending e).
