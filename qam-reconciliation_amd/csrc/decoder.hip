@@ -44,9 +44,8 @@ __device__ __forceinline__ void st_msg(double *p, double v) {
     else *p = v;
 }
 
-// Row `row` (wave-uniform) of a frame-innermost array: a scalar base, so every access
-// is `global_load ... v_off, s[base]` with one 32-bit lane offset (f * 8) shared by all
-// rows instead of a 64-bit address per access (frees ~2 VGPRs per live message).
+// Row `row` (wave-uniform) of a frame-innermost array: the row offset is computed in
+// scalar registers; lanes add their byte offset f * sizeof(T).
 template <typename T>
 __device__ __forceinline__ T *row_ptr(T *base, int row, int ld) {
     return base + (size_t)(uint32_t)__builtin_amdgcn_readfirstlane(row) * (size_t)ld;
