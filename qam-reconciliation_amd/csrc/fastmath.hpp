@@ -84,10 +84,16 @@ __host__ __device__ __forceinline__ double h_softplus_neg(double t, const MathTa
     const uint64_t tb = __builtin_bit_cast(uint64_t, t);
     const uint32_t thi = (t > 37.5) ? 0x4042C000u : (uint32_t)(tb >> 32);
     const double tc = __builtin_bit_cast(double, ((uint64_t)thi << 32) | (uint32_t)tb);
-    const double kd = __builtin_rint(tc * -kInvL);
+    // k = rint(-t 256/ln2) by the 1.5*2^52 shift: the low word of kb is k (two's
+    // complement, |k| <= 13850) and kd = kb - shift is k as a double -- one fma and one
+    // add instead of mul + rndne + cvt (a near-tie may pick the neighbouring k; r then
+    // exceeds ln2/512 by an ulp, which the polynomial absorbs).  NaN: k = 0, kd = NaN.
+    constexpr double kShift = 0x1.8p52;
+    const double kb = __builtin_fma(tc, -kInvL, kShift);
+    const int k = (int)(uint32_t)__builtin_bit_cast(uint64_t, kb);
+    const double kd = kb - kShift;
     double r = __builtin_fma(kd, -kL2Hi, -tc);
     r = __builtin_fma(kd, -kL2Lo, r);
-    const int k = (int)kd;                              // in [-13850, 0] (0 for NaN)
     const double s = T.exp2j[k & (kExpN - 1)];
     double p = __builtin_fma(r, 1.0 / 24.0, 1.0 / 6.0); // expm1(r) = r + r^2 (1/2 + r/6 + r^2/24)
     p = __builtin_fma(p, r, 0.5);
@@ -95,9 +101,14 @@ __host__ __device__ __forceinline__ double h_softplus_neg(double t, const MathTa
     const double e = __builtin_ldexp(__builtin_fma(s, p, s), k >> kExpBits);
     const double u = 1.0 + e;                           // in (1, 2] or NaN
     const uint32_t hi32 = (uint32_t)(__builtin_bit_cast(uint64_t, u) >> 32);
-    uint32_t i = (hi32 >> (20 - kLogBits)) - (0x3ff00000u >> (20 - kLogBits));
-    i = (i < (uint32_t)kLogN) ? i : (uint32_t)kLogN;    // in range for NaN too
+    // i in [0, 512] for u in [1, 2]; a NaN u gives an index past the table, whose LDS
+    // read returns whatever (LDS reads do not fault) -- q and h are NaN regardless.
+    const uint32_t i = (hi32 >> (20 - kLogBits)) - (0x3ff00000u >> (20 - kLogBits));
+#ifdef __HIP_DEVICE_COMPILE__
     const double2 c = T.logt[i];
+#else
+    const double2 c = T.logt[(i < (uint32_t)kLogN) ? i : (uint32_t)kLogN];  // host: stay in bounds
+#endif
     const double q = __builtin_fma(u, c.x, -1.0);
     // log1p(q) = q + q^2 (-1/2 + q/3 - q^2/4 + q^3/5): |q| < 2^-9, the truncation
     // q^6/6 < 2^-56 (absolute; h itself carries the 2^-53 rounding of 1 + e)
