@@ -270,7 +270,9 @@ def main():
             bc0, _ = check_class_bytes(vid, cid, 7, fr_c)
             bc1, _ = check_class_bytes(vid, cid, 7, max(batch.B - fr_c, 0))
             bytes_launch = (bc0 + bc1) / 2 + (var_sweep_bytes(V_, E_, fr_c) + var_sweep_bytes(V_, E_, fr_v)) / 2
-            kname, kkey = "k_fused<7,Normal> (check sweep of one frame half + variable sweep of the other)", "fused_d7"
+            kname = ("k_fused_eps<7,Normal> (exp-domain" if qamr._lib.tune_get("eps") else "k_fused<7,Normal> (exact") + \
+                " check sweep of one frame half + variable sweep of the other)"
+            kkey = "fused_d7"
         elif "check_d7" in kstats:
             bytes_launch, _ = check_class_bytes(vid, cid, 7, batch.B)
             kname, kkey = "k_check<7,Normal> (degree-7 check-node sweep)", "check_d7"
@@ -285,7 +287,7 @@ def main():
                 try:
                     t = json.load(open(pmc))
                     if t.get("workload") == args.workload and int(t.get("batch", -1)) == batch.B \
-                            and t.get("kernel_key") == kkey:
+                            and t.get("kernel_key") == kkey and kname.startswith(t.get("kernel", "?").split("<")[0] + "<"):
                         traffic = t.get("hbm_bytes_per_launch")
                 except Exception:
                     traffic = None

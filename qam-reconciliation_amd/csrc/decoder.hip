@@ -79,6 +79,7 @@ struct CheckArgs {
     Geom g;
     unsigned nbx;  // blocks along the check axis
     const MathTables *gtab;
+    double eps_max;      // exp-domain inputs: |m| <= eps_max (<= kEpsMax)
 };
 
 // One variable sweep over the frame columns [f_off, f_off + ny*ft).
@@ -125,12 +126,39 @@ struct CheckIn {
     }
 };
 
+// decoder.pyx:322-369 for one check, the reference's arithmetic (fastmath.hpp::box_plus_fast):
+// F[i] = bp(F[i-1], m[i]); the backward values B[i] = bp(B[i+1], m[i]) are consumed as
+// they are produced (out_i = bp(F[i-1], B[i+1])): the same operands as
+// decoder.pyx:341-367, one live B instead of D.  Lane byte offset b8 = f * 8.
+template <int D, bool NT>
+__device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m)[D], int base, uint8_t sb, uint32_t b8,
+                                            const MathTables &tab) {
+    const int ld = a.ld;
+    const double s = sb ? -1.0 : 1.0;
+    double F[D - 1];
+    F[0] = m[0];
+#pragma unroll
+    for (int i = 1; i < D - 1; ++i) F[i] = box_plus_fast(F[i - 1], m[i], tab);
+    st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + D - 1], ld), b8), s * F[D - 2]);
+    double Bn = m[D - 1];
+#pragma unroll
+    for (int i = D - 2; i > 0; --i) {
+        st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), s * box_plus_fast(F[i - 1], Bn, tab));
+        Bn = box_plus_fast(Bn, m[i], tab);
+    }
+    st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base], ld), b8), s * Bn);
+}
+
 // One lane = one (check, frame); each thread walks `per` checks of one degree class.
 // decoder.pyx:322-369 (F/B recursion) with the parity test of decoder.pyx:235-257
 // fused on the posteriors it gathers anyway.  Software-pipelined: the posterior
 // gathers of check j+1 are issued before the box-plus arithmetic of check j, so
 // each wave keeps its own loads in flight under its VALU work.
-template <int D, int MODE, bool NT>
+// EPS: the update runs in the exp domain (fastmath.hpp::check_node_eps, ~2.4x fewer
+// VALU instructions) in every lane whose inputs are all in its domain, the exact path
+// in the others; a wave whose lanes agree runs one path only (the other is skipped
+// under an empty exec mask), and a frame's result never depends on its wave-mates.
+template <int D, int MODE, bool NT, bool EPS>
 __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, unsigned by, const MathTables &tab) {
     const int ft = 1 << a.g.lft;
     const int nsub = 256 >> a.g.lft;
@@ -165,24 +193,23 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
         if (more) nx.load(a, cn, f);
         if (MODE != kFirst) bad |= (par == 1u) ? 1u : 0u;  // satisfied iff (parity ^ 1) != 0
         if (MODE != kParityOnly) {
-            // F[i] = bp(F[i-1], m[i]); the backward values B[i] = bp(B[i+1], m[i]) are
-            // consumed as they are produced (out_i = bp(F[i-1], B[i+1])): the same
-            // operands as decoder.pyx:341-367, one live B instead of D.
-            const int base = cur.base;
             const uint32_t b8 = (uint32_t)f * 8u;
-            const double s = cur.sb ? -1.0 : 1.0;
-            double F[D - 1];
-            F[0] = m[0];
+            if constexpr (EPS) {
+                bool in = true;
 #pragma unroll
-            for (int i = 1; i < D - 1; ++i) F[i] = box_plus_fast(F[i - 1], m[i], tab);
-            st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + D - 1], ld), b8), s * F[D - 2]);
-            double Bn = m[D - 1];
-#pragma unroll
-            for (int i = D - 2; i > 0; --i) {
-                st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), s * box_plus_fast(F[i - 1], Bn, tab));
-                Bn = box_plus_fast(Bn, m[i], tab);
+                for (int i = 0; i < D; ++i) in &= eps_ok(m[i], a.eps_max);
+                // per lane: a wave whose lanes all agree runs one path (execz skips the other)
+                if (in || !act) {  // stopped lanes never force the exact path
+                    const int base = cur.base;
+                    check_node_eps<D>(m, cur.sb, tab, [&](int i, double v) {
+                        st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), v);
+                    });
+                } else {
+                    check_exact<D, NT>(a, m, cur.base, cur.sb, b8, tab);
+                }
+            } else {
+                check_exact<D, NT>(a, m, cur.base, cur.sb, b8, tab);
             }
-            st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base], ld), b8), s * Bn);
         }
         if (!more) break;
         ci = cn;
@@ -218,11 +245,11 @@ __device__ __forceinline__ void var_block(const VarArgs &a, unsigned bx, unsigne
     }
 }
 
-template <int D, int MODE, bool NT>
+template <int D, int MODE, bool NT, bool EPS>
 __global__ void __launch_bounds__(256) k_check(CheckArgs a) {
     __shared__ MathTables tab;
     if (MODE != kParityOnly) stage_math_tables(&tab, a.gtab);
-    check_block<D, MODE, NT>(a, blockIdx.x, blockIdx.y, tab);
+    check_block<D, MODE, NT, EPS>(a, blockIdx.x, blockIdx.y, tab);
 }
 
 template <bool INIT, bool NT>
@@ -231,32 +258,49 @@ __global__ void __launch_bounds__(256) k_var(VarArgs a) {
 }
 
 // One launch = the check sweep of one frame half and the variable sweep of the
-// other (they never touch the same frame columns).  The check sweep is fp64-VALU
-// bound and the variable sweep HBM bound: interleaving their workgroups (evenly
-// spread over the 1-D grid, in proportion to their counts) lets the dispatcher
-// co-schedule them on every CU, so the message stream of one hides under the
-// transcendental arithmetic of the other.
-// Occupancy floor of the fused sweep: 6 waves/SIMD (80 VGPRs, a few spilled bytes)
-// beats the 4 waves the software-pipelined check sweep would get unconstrained
-// (3.19 vs 3.28 (5 waves) / 3.23 (7 waves) ms per launch on MI355X;
-// scripts/exp_build.sh QR_FUSED_WAVES=n).
+// other (they never touch the same frame columns).  The check sweep is VALU heavy
+// and the variable sweep HBM bound: interleaving their workgroups (evenly spread
+// over the 1-D grid, in proportion to their counts) lets the dispatcher co-schedule
+// them on every CU, so the message stream of one hides under the arithmetic of the
+// other.
+// Occupancy floors (amdgpu_waves_per_eu, MI355X, scripts/exp_build.sh):
+//   exact box-plus (QR_FUSED_WAVES, 6 waves/SIMD = 80 VGPRs): 3.09 ms per launch vs
+//     3.14 (5 waves) / 3.26 (4 waves);
+//   exp domain (QR_FUSED_EPS_WAVES, 5 waves = 96 VGPRs, no spill): 2.73 ms vs 3.21
+//     (6 waves, 80 B spilled per lane inside the loop) / 2.94 (4 waves).
 #ifndef QR_FUSED_WAVES
 #define QR_FUSED_WAVES 6
 #endif
-#define QR_FUSED_ATTR __attribute__((amdgpu_waves_per_eu(QR_FUSED_WAVES, 8)))
-template <int D, int MODE, bool NT>
-__global__ void __launch_bounds__(256) QR_FUSED_ATTR k_fused(CheckArgs ca, VarArgs va, unsigned nb_check, unsigned nb_total) {
-    __shared__ MathTables tab;
+#ifndef QR_FUSED_EPS_WAVES
+#define QR_FUSED_EPS_WAVES 5
+#endif
+template <int D, int MODE, bool NT, bool EPS>
+__device__ __forceinline__ void fused_body(const CheckArgs &ca, const VarArgs &va, unsigned nb_check,
+                                           unsigned nb_total, MathTables &tab) {
     const unsigned b = blockIdx.x;
     const unsigned c0 = (unsigned)(((uint64_t)b * nb_check) / nb_total);
     const unsigned c1 = (unsigned)(((uint64_t)(b + 1) * nb_check) / nb_total);
     if (c1 > c0) {  // block-uniform branch
         stage_math_tables(&tab, ca.gtab);
-        check_block<D, MODE, NT>(ca, c0 % ca.nbx, c0 / ca.nbx, tab);
+        check_block<D, MODE, NT, EPS>(ca, c0 % ca.nbx, c0 / ca.nbx, tab);
     } else {
         const unsigned vi = b - c0;
         var_block<false, NT>(va, vi % va.nbx, vi / va.nbx);
     }
+}
+
+template <int D, int MODE, bool NT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QR_FUSED_WAVES, 8)))
+k_fused(CheckArgs ca, VarArgs va, unsigned nb_check, unsigned nb_total) {
+    __shared__ MathTables tab;
+    fused_body<D, MODE, NT, false>(ca, va, nb_check, nb_total, tab);
+}
+
+template <int D, int MODE, bool NT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QR_FUSED_EPS_WAVES, 8)))
+k_fused_eps(CheckArgs ca, VarArgs va, unsigned nb_check, unsigned nb_total) {
+    __shared__ MathTables tab;
+    fused_body<D, MODE, NT, true>(ca, va, nb_check, nb_total, tab);
 }
 
 // Runtime-degree fallback for check degrees above the templated range (2..16).
@@ -362,7 +406,7 @@ static DecodeWs carve(const qr_code *code, int ld, void *base) {
 
 // Runtime tuning knobs (qr_tune_set); defaults picked by scripts/tune.py on MI355X.
 struct Tuning {
-    std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{2};
+    std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{2}, eps{1}, eps_max{40};
 };
 static Tuning g_tune;
 
@@ -405,6 +449,7 @@ struct Plan {
         const int64_t per_block = (int64_t)a.g.per * (256 >> a.g.lft);
         a.nbx = (unsigned)((cls.n + per_block - 1) / per_block);
         a.gtab = code->d_mtab;
+        a.eps_max = std::min<double>(g_tune.eps_max.load(), kEpsMax);
         return a;
     }
     VarArgs var_args(int f0, int f1) const {
@@ -433,18 +478,26 @@ struct Plan {
         default: handled = false;                                                                            \
     }
 
+// Exp-domain check update on (knob eps) for the sweeps that compute messages.
+static bool use_eps(int mode) { return mode != kParityOnly && g_tune.eps.load() != 0; }
+
 template <int MODE, bool NT>
 static int launch_check_class(const Plan &P, const DegreeClass &cls, const double *post_in, uint8_t *unsat, int f0,
                               int f1) {
     const CheckArgs a = P.check_args(cls, post_in, unsat, f0, f1);
+    const bool eps = use_eps(MODE);
     dim3 grid(a.nbx, (unsigned)((f1 - f0) >> a.g.lft));
     ProfScope ps(profiling_on() ? std::string(MODE == kParityOnly ? "parity_d" : MODE == kFirst ? "check1_d" : "check_d") +
                                       std::to_string(cls.degree)
                                 : std::string(),
                  P.s);
-#define QR_CASE(DD)                                          \
-    case DD:                                                 \
-        k_check<DD, MODE, NT><<<grid, 256, 0, P.s>>>(a);     \
+#define QR_CASE(DD)                                                  \
+    case DD:                                                         \
+        if (eps) {                                                   \
+            k_check<DD, MODE, NT, true><<<grid, 256, 0, P.s>>>(a);   \
+        } else {                                                     \
+            k_check<DD, MODE, NT, false><<<grid, 256, 0, P.s>>>(a);  \
+        }                                                            \
         break;
     bool handled = true;
     QR_DEG_SWITCH(cls.degree, QR_CASE, handled)
@@ -481,17 +534,24 @@ static int launch_var(const Plan &P, int f0, int f1) {
 template <int MODE, bool NT>
 static int launch_fused_nt(const Plan &P, const DegreeClass &cls, uint8_t *unsat, int cf0, int cf1, int vf0, int vf1) {
     const CheckArgs ca = P.check_args(cls, P.post, unsat, cf0, cf1);
+    const bool eps = use_eps(MODE);
     const VarArgs va = P.var_args(vf0, vf1);
     const unsigned nbc = ca.nbx * (unsigned)((cf1 - cf0) >> ca.g.lft);
     const unsigned nbv = va.nbx * (unsigned)((vf1 - vf0) >> va.g.lft);
-    ProfScope ps(profiling_on() ? std::string("fused_d") + std::to_string(cls.degree) : std::string(), P.s);
-#define QR_CASE(DD)                                                                 \
-    case DD:                                                                        \
-        k_fused<DD, MODE, NT><<<nbc + nbv, 256, 0, P.s>>>(ca, va, nbc, nbc + nbv); \
-        break;
     bool handled = true;
-    QR_DEG_SWITCH(cls.degree, QR_CASE, handled)
+    {
+        ProfScope ps(profiling_on() ? std::string("fused_d") + std::to_string(cls.degree) : std::string(), P.s);
+#define QR_CASE(DD)                                                                           \
+    case DD:                                                                                  \
+        if (eps) {                                                                            \
+            k_fused_eps<DD, MODE, NT><<<nbc + nbv, 256, 0, P.s>>>(ca, va, nbc, nbc + nbv);   \
+        } else {                                                                              \
+            k_fused<DD, MODE, NT><<<nbc + nbv, 256, 0, P.s>>>(ca, va, nbc, nbc + nbv);       \
+        }                                                                                     \
+        break;
+        QR_DEG_SWITCH(cls.degree, QR_CASE, handled)
 #undef QR_CASE
+    }
     if (!handled) return set_error(QR_EUNSUPPORTED, "fused launch needs check degree <= 16");
     QR_LAUNCH_CHECK();
     return QR_OK;
@@ -779,6 +839,7 @@ int qr_tune_set(const char *name, int64_t value) {
     std::atomic<int> *k = n == "check_ft" ? &g_tune.check_ft : n == "check_per" ? &g_tune.check_per
                         : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
                         : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
+                        : n == "eps"      ? &g_tune.eps      : n == "eps_max"   ? &g_tune.eps_max
                         : n == "demap_fast" ? &g_demap_fast : nullptr;
     if (!k) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     if (value < 0 || value > 4096) return set_error(QR_EVALUE, "tuning value out of range");
@@ -791,6 +852,7 @@ int qr_tune_get(const char *name, int64_t *value) {
     const std::atomic<int> *k = n == "check_ft" ? &g_tune.check_ft : n == "check_per" ? &g_tune.check_per
                               : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
                               : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
+                              : n == "eps"      ? &g_tune.eps      : n == "eps_max"   ? &g_tune.eps_max
                               : n == "demap_fast" ? &g_demap_fast : nullptr;
     if (!k || !value) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     *value = k->load();

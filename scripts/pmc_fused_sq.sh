@@ -4,7 +4,7 @@ import csv,glob,collections
 agg=collections.defaultdict(list)
 for f in sorted(glob.glob("gpurun_out/prof_fusedpmc/pmc*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        if r["Kernel_Name"].startswith("void qr::k_fused<7, 1"):
+        if r["Kernel_Name"].startswith("void qr::k_fused_eps<7, 1"):
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 for c,v in agg.items(): print(c, "%.4g" % (sum(v)/len(v)), len(v))
 PY

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise a scripts/profile_session.sh output directory.
 
-    python scripts/summarize_profile.py gpurun_out/prof_r1 [--kernel k_fused<7, 1, true>]
+    python scripts/summarize_profile.py gpurun_out/prof_r1 [--kernel k_fused_eps<7, 1, true>]
 
 Writes <dir>/summary.md (per-kernel time from --kernel-trace --stats, PMC counters
 per launch) and <dir>/pmc_traffic.json: HBM bytes per launch of the dominant
@@ -25,7 +25,7 @@ def short(name):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--kernel", default="k_fused<7, 1, true>")
+    ap.add_argument("--kernel", default="k_fused_eps<7, 1, true>")
     ap.add_argument("--kernel-key", default="fused_d7")
     ap.add_argument("--workload", default="dvbs2_4pam")
     ap.add_argument("--batch", type=int, default=4096)

@@ -202,3 +202,42 @@ def test_device_api_layout_and_properties(gpu):
     perm = np.random.default_rng(0).permutation(B)
     s_p, i_p, f_p = dec.decode_batch(L[perm], S[perm], 50)
     assert np.array_equal(s_p, s_h[perm]) and np.array_equal(i_p, i_h[perm]) and np.array_equal(f_p, f_h[perm])
+
+
+def test_exp_domain_and_exact_paths(gpu):
+    """The exp-domain check update (default) and the exact box-plus path (knob eps=0)
+    both match the oracle; frames whose check inputs leave the exp domain (|m| > 700,
+    inf) take the exact path per lane, so results do not depend on which frames share
+    a wavefront (permuting frames permutes results bit for bit)."""
+    from qamr import _lib, codes
+
+    vid, cid = codes.regular_code(1008)
+    dec = _decoder(vid, cid)
+    orc = O.OracleCode(vid, cid)
+    rng = np.random.default_rng(7)
+    B = 192
+    sig = rng.uniform(0.55, 1.0, B)[:, None]
+    word = rng.integers(0, 2, (B, 1008)).astype(np.uint8)
+    synd = np.stack([orc.eval_syndrome(w) for w in word])
+    llr = 2 / sig ** 2 * ((1 - 2.0 * word) + sig * rng.standard_normal((B, 1008)))
+    big = rng.choice(B, 40, replace=False)
+    llr[big[:20]] *= 150.0                                   # |LLR| in the hundreds..thousands
+    llr[big[20:], :30] *= 1e4                                 # a few huge inputs per frame
+    llr[big[0], 5] = np.inf
+    s2, i2, f2 = orc.decode_batch(llr, synd, 50)
+    try:
+        res = {}
+        for eps in (1, 0):
+            _lib.tune_set("eps", eps)
+            s1, i1, f1 = dec.decode_batch(llr, synd, 50)
+            assert np.array_equal(s1, s2) and np.array_equal(i1, i2), eps
+            assert np.array_equal(f1 < 0, f2 < 0), eps
+            assert_llr_close(f1, f2)
+            res[eps] = f1
+        _lib.tune_set("eps", 1)
+        perm = rng.permutation(B)
+        s_p, i_p, f_p = dec.decode_batch(llr[perm], synd[perm], 50)
+        assert np.array_equal(s_p, s2[perm]) and np.array_equal(i_p, i2[perm])
+        assert np.array_equal(f_p.view(np.int64), res[1][perm].view(np.int64))
+    finally:
+        _lib.tune_set("eps", 1)
