@@ -261,6 +261,7 @@ def main():
             if n:
                 kstats[k] = {"avg_us": 1e3 * ms / n, "launches": n, "total_ms": ms}
         V_, E_ = dec.vnum, dec.ednum
+        math_mode = int(qamr._lib.tune_get("math"))
         if "fused_d7" in kstats:
             # split schedule: one launch = check sweep of one frame half + variable sweep of the other
             half = batch.ld // 2
@@ -270,8 +271,8 @@ def main():
             bc0, _ = check_class_bytes(vid, cid, 7, fr_c)
             bc1, _ = check_class_bytes(vid, cid, 7, max(batch.B - fr_c, 0))
             bytes_launch = (bc0 + bc1) / 2 + (var_sweep_bytes(V_, E_, fr_c) + var_sweep_bytes(V_, E_, fr_v)) / 2
-            kname = ("k_fused_eps<7,Normal> (exp-domain" if qamr._lib.tune_get("eps") else "k_fused<7,Normal> (exact") + \
-                " check sweep of one frame half + variable sweep of the other)"
+            ar = {0: "kStrict", 1: "kFast", 2: "kEps"}.get(math_mode, "?")
+            kname = f"k_fused<7,Normal,{ar}> (check sweep of one frame half + variable sweep of the other)"
             kkey = "fused_d7"
         elif "check_d7" in kstats:
             bytes_launch, _ = check_class_bytes(vid, cid, 7, batch.B)
@@ -287,7 +288,7 @@ def main():
                 try:
                     t = json.load(open(pmc))
                     if t.get("workload") == args.workload and int(t.get("batch", -1)) == batch.B \
-                            and t.get("kernel_key") == kkey and kname.startswith(t.get("kernel", "?").split("<")[0] + "<"):
+                            and t.get("kernel_key") == kkey and t.get("math") == math_mode:
                         traffic = t.get("hbm_bytes_per_launch")
                 except Exception:
                     traffic = None

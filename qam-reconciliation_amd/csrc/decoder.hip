@@ -25,11 +25,32 @@
 #include <atomic>
 
 #include "fastmath.hpp"
+#include "glibc_math.hpp"
 #include "qamr_internal.hpp"
 
 namespace qr {
 
 enum CheckMode { kFirst = 0, kNormal = 1, kParityOnly = 2 };
+
+// Check-node arithmetic (knob "math"):
+//   kStrict -- the reference's box-plus bit for bit: glibc exp/log restated
+//              (glibc_math.hpp), so every message, posterior and output LAPPR is
+//              identical to the reference's;
+//   kFast   -- box-plus with the table h(t) of fastmath.hpp (<= ulp(1) per h);
+//   kEps    -- the exp-domain update of fastmath.hpp (lanes with inputs beyond
+//              eps_max take the kFast box-plus).
+enum MathMode { kStrict = 0, kFast = 1, kEps = 2 };
+
+template <int AR>
+struct Arith {  // kFast, kEps: MathTables (10 KiB) in LDS
+    using Tab = MathTables;
+    static __device__ __forceinline__ double bp(double a, double b, const Tab &T) { return box_plus_fast(a, b, T); }
+};
+template <>
+struct Arith<kStrict> {  // GlibcTables (4 KiB) in LDS
+    using Tab = GlibcTables;
+    static __device__ __forceinline__ double bp(double a, double b, const Tab &T) { return box_plus_strict(a, b, T); }
+};
 
 // Edge-message access: NT = non-temporal (streamed once per sweep; keeps the
 // re-read posteriors resident in L2/MALL instead of the message stream).
@@ -79,6 +100,7 @@ struct CheckArgs {
     Geom g;
     unsigned nbx;  // blocks along the check axis
     const MathTables *gtab;
+    const GlibcTables *gglibc;
     double eps_max;      // exp-domain inputs: |m| <= eps_max (<= kEpsMax)
 };
 
@@ -93,6 +115,12 @@ struct VarArgs {
     Geom g;
     unsigned nbx;
 };
+
+template <int AR>
+__device__ __forceinline__ void stage_tables(typename Arith<AR>::Tab *lds, const CheckArgs &a) {
+    if constexpr (AR == kStrict) stage_glibc_tables(lds, a.gglibc);
+    else stage_math_tables(lds, a.gtab);
+}
 
 // The inputs of one check update: gathered posteriors, own c2v messages, syndrome bit.
 // Prefetch depth: the gathered posteriors of check j+1 are always issued before the
@@ -126,25 +154,25 @@ struct CheckIn {
     }
 };
 
-// decoder.pyx:322-369 for one check, the reference's arithmetic (fastmath.hpp::box_plus_fast):
+// decoder.pyx:322-369 for one check with the box-plus of Arith<AR>:
 // F[i] = bp(F[i-1], m[i]); the backward values B[i] = bp(B[i+1], m[i]) are consumed as
 // they are produced (out_i = bp(F[i-1], B[i+1])): the same operands as
 // decoder.pyx:341-367, one live B instead of D.  Lane byte offset b8 = f * 8.
-template <int D, bool NT>
+template <int AR, int D, bool NT>
 __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m)[D], int base, uint8_t sb, uint32_t b8,
-                                            const MathTables &tab) {
+                                            const typename Arith<AR>::Tab &tab) {
     const int ld = a.ld;
     const double s = sb ? -1.0 : 1.0;
     double F[D - 1];
     F[0] = m[0];
 #pragma unroll
-    for (int i = 1; i < D - 1; ++i) F[i] = box_plus_fast(F[i - 1], m[i], tab);
+    for (int i = 1; i < D - 1; ++i) F[i] = Arith<AR>::bp(F[i - 1], m[i], tab);
     st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + D - 1], ld), b8), s * F[D - 2]);
     double Bn = m[D - 1];
 #pragma unroll
     for (int i = D - 2; i > 0; --i) {
-        st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), s * box_plus_fast(F[i - 1], Bn, tab));
-        Bn = box_plus_fast(Bn, m[i], tab);
+        st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), s * Arith<AR>::bp(F[i - 1], Bn, tab));
+        Bn = Arith<AR>::bp(Bn, m[i], tab);
     }
     st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base], ld), b8), s * Bn);
 }
@@ -158,8 +186,9 @@ __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m
 // VALU instructions) in every lane whose inputs are all in its domain, the exact path
 // in the others; a wave whose lanes agree runs one path only (the other is skipped
 // under an empty exec mask), and a frame's result never depends on its wave-mates.
-template <int D, int MODE, bool NT, bool EPS>
-__device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, unsigned by, const MathTables &tab) {
+template <int D, int MODE, bool NT, int AR>
+__device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, unsigned by,
+                                            const typename Arith<AR>::Tab &tab) {
     const int ft = 1 << a.g.lft;
     const int nsub = 256 >> a.g.lft;
     const int ld = a.ld;
@@ -194,7 +223,7 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
         if (MODE != kFirst) bad |= (par == 1u) ? 1u : 0u;  // satisfied iff (parity ^ 1) != 0
         if (MODE != kParityOnly) {
             const uint32_t b8 = (uint32_t)f * 8u;
-            if constexpr (EPS) {
+            if constexpr (AR == kEps) {
                 bool in = true;
 #pragma unroll
                 for (int i = 0; i < D; ++i) in &= eps_ok(m[i], a.eps_max);
@@ -205,10 +234,10 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
                         st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), v);
                     });
                 } else {
-                    check_exact<D, NT>(a, m, cur.base, cur.sb, b8, tab);
+                    check_exact<kFast, D, NT>(a, m, cur.base, cur.sb, b8, tab);
                 }
             } else {
-                check_exact<D, NT>(a, m, cur.base, cur.sb, b8, tab);
+                check_exact<AR, D, NT>(a, m, cur.base, cur.sb, b8, tab);
             }
         }
         if (!more) break;
@@ -245,11 +274,11 @@ __device__ __forceinline__ void var_block(const VarArgs &a, unsigned bx, unsigne
     }
 }
 
-template <int D, int MODE, bool NT, bool EPS>
+template <int D, int MODE, bool NT, int AR>
 __global__ void __launch_bounds__(256) k_check(CheckArgs a) {
-    __shared__ MathTables tab;
-    if (MODE != kParityOnly) stage_math_tables(&tab, a.gtab);
-    check_block<D, MODE, NT, EPS>(a, blockIdx.x, blockIdx.y, tab);
+    __shared__ typename Arith<AR>::Tab tab;
+    if (MODE != kParityOnly) stage_tables<AR>(&tab, a);
+    check_block<D, MODE, NT, AR>(a, blockIdx.x, blockIdx.y, tab);
 }
 
 template <bool INIT, bool NT>
@@ -268,60 +297,57 @@ __global__ void __launch_bounds__(256) k_var(VarArgs a) {
 //     3.14 (5 waves) / 3.26 (4 waves);
 //   exp domain (QR_FUSED_EPS_WAVES, 5 waves = 96 VGPRs, no spill): 2.73 ms vs 3.21
 //     (6 waves, 80 B spilled per lane inside the loop) / 2.94 (4 waves).
+//   strict box-plus (QR_FUSED_STRICT_WAVES): to be tuned.
 #ifndef QR_FUSED_WAVES
 #define QR_FUSED_WAVES 6
 #endif
 #ifndef QR_FUSED_EPS_WAVES
 #define QR_FUSED_EPS_WAVES 5
 #endif
-template <int D, int MODE, bool NT, bool EPS>
-__device__ __forceinline__ void fused_body(const CheckArgs &ca, const VarArgs &va, unsigned nb_check,
-                                           unsigned nb_total, MathTables &tab) {
+#ifndef QR_FUSED_STRICT_WAVES
+#define QR_FUSED_STRICT_WAVES 5
+#endif
+template <int AR>
+struct FusedWaves {
+    static constexpr int value = AR == kStrict ? QR_FUSED_STRICT_WAVES : AR == kEps ? QR_FUSED_EPS_WAVES : QR_FUSED_WAVES;
+};
+
+template <int D, int MODE, bool NT, int AR>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FusedWaves<AR>::value, 8)))
+k_fused(CheckArgs ca, VarArgs va, unsigned nb_check, unsigned nb_total) {
+    __shared__ typename Arith<AR>::Tab tab;
     const unsigned b = blockIdx.x;
     const unsigned c0 = (unsigned)(((uint64_t)b * nb_check) / nb_total);
     const unsigned c1 = (unsigned)(((uint64_t)(b + 1) * nb_check) / nb_total);
     if (c1 > c0) {  // block-uniform branch
-        stage_math_tables(&tab, ca.gtab);
-        check_block<D, MODE, NT, EPS>(ca, c0 % ca.nbx, c0 / ca.nbx, tab);
+        stage_tables<AR>(&tab, ca);
+        check_block<D, MODE, NT, AR>(ca, c0 % ca.nbx, c0 / ca.nbx, tab);
     } else {
         const unsigned vi = b - c0;
         var_block<false, NT>(va, vi % va.nbx, vi / va.nbx);
     }
 }
 
-template <int D, int MODE, bool NT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QR_FUSED_WAVES, 8)))
-k_fused(CheckArgs ca, VarArgs va, unsigned nb_check, unsigned nb_total) {
-    __shared__ MathTables tab;
-    fused_body<D, MODE, NT, false>(ca, va, nb_check, nb_total, tab);
-}
-
-template <int D, int MODE, bool NT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QR_FUSED_EPS_WAVES, 8)))
-k_fused_eps(CheckArgs ca, VarArgs va, unsigned nb_check, unsigned nb_total) {
-    __shared__ MathTables tab;
-    fused_body<D, MODE, NT, true>(ca, va, nb_check, nb_total, tab);
-}
-
 // Runtime-degree fallback for check degrees above the templated range (2..16).
 constexpr int kMaxGenericDeg = 64;
 
+template <int AR>
 __device__ __forceinline__ void check_update_generic(int d, const double *m, double *out, double s,
-                                                     const MathTables &tab) {
+                                                     const typename Arith<AR>::Tab &tab) {
     double F[kMaxGenericDeg], Bk[kMaxGenericDeg];
     F[0] = m[0];
-    for (int i = 1; i < d - 1; ++i) F[i] = box_plus_fast(F[i - 1], m[i], tab);
+    for (int i = 1; i < d - 1; ++i) F[i] = Arith<AR>::bp(F[i - 1], m[i], tab);
     Bk[d - 1] = m[d - 1];
-    for (int i = d - 2; i > 0; --i) Bk[i] = box_plus_fast(Bk[i + 1], m[i], tab);
+    for (int i = d - 2; i > 0; --i) Bk[i] = Arith<AR>::bp(Bk[i + 1], m[i], tab);
     out[0] = s * Bk[1];
-    for (int i = 1; i < d - 1; ++i) out[i] = s * box_plus_fast(F[i - 1], Bk[i + 1], tab);
+    for (int i = 1; i < d - 1; ++i) out[i] = s * Arith<AR>::bp(F[i - 1], Bk[i + 1], tab);
     out[d - 1] = s * F[d - 2];
 }
 
-template <int MODE>
+template <int MODE, int AR>
 __global__ void __launch_bounds__(256) k_check_generic(CheckArgs a) {
-    __shared__ MathTables tab;
-    if (MODE != kParityOnly) stage_math_tables(&tab, a.gtab);
+    __shared__ typename Arith<AR>::Tab tab;
+    if (MODE != kParityOnly) stage_tables<AR>(&tab, a);
     const int ft = 1 << a.g.lft;
     const int nsub = 256 >> a.g.lft;
     const int ld = a.ld;
@@ -346,7 +372,7 @@ __global__ void __launch_bounds__(256) k_check_generic(CheckArgs a) {
         }
         if (MODE != kFirst) bad |= (par == 1u) ? 1u : 0u;
         if (MODE == kParityOnly) continue;
-        check_update_generic(d, m, out, sb ? -1.0 : 1.0, tab);
+        check_update_generic<AR>(d, m, out, sb ? -1.0 : 1.0, tab);
         for (int i = 0; i < d; ++i) a.c2v[(size_t)a.chk_edge[base + i] * ld + f] = out[i];
     }
     if (MODE != kFirst && bad) a.unsat[f] = 1;
@@ -406,7 +432,7 @@ static DecodeWs carve(const qr_code *code, int ld, void *base) {
 
 // Runtime tuning knobs (qr_tune_set); defaults picked by scripts/tune.py on MI355X.
 struct Tuning {
-    std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{2}, eps{1}, eps_max{40};
+    std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{2}, math{kStrict}, eps_max{40};
 };
 static Tuning g_tune;
 
@@ -449,6 +475,7 @@ struct Plan {
         const int64_t per_block = (int64_t)a.g.per * (256 >> a.g.lft);
         a.nbx = (unsigned)((cls.n + per_block - 1) / per_block);
         a.gtab = code->d_mtab;
+        a.gglibc = code->d_gtab;
         a.eps_max = std::min<double>(g_tune.eps_max.load(), kEpsMax);
         return a;
     }
@@ -478,31 +505,35 @@ struct Plan {
         default: handled = false;                                                                            \
     }
 
-// Exp-domain check update on (knob eps) for the sweeps that compute messages.
-static bool use_eps(int mode) { return mode != kParityOnly && g_tune.eps.load() != 0; }
+// Arithmetic of the check launches (knob math); parity-only sweeps need no tables.
+static int math_mode(int mode) {
+    const int m = g_tune.math.load();
+    return mode == kParityOnly ? kFast : (m == kFast || m == kEps) ? m : kStrict;
+}
 
 template <int MODE, bool NT>
 static int launch_check_class(const Plan &P, const DegreeClass &cls, const double *post_in, uint8_t *unsat, int f0,
                               int f1) {
     const CheckArgs a = P.check_args(cls, post_in, unsat, f0, f1);
-    const bool eps = use_eps(MODE);
+    const int ar = math_mode(MODE);
     dim3 grid(a.nbx, (unsigned)((f1 - f0) >> a.g.lft));
     ProfScope ps(profiling_on() ? std::string(MODE == kParityOnly ? "parity_d" : MODE == kFirst ? "check1_d" : "check_d") +
                                       std::to_string(cls.degree)
                                 : std::string(),
                  P.s);
-#define QR_CASE(DD)                                                  \
-    case DD:                                                         \
-        if (eps) {                                                   \
-            k_check<DD, MODE, NT, true><<<grid, 256, 0, P.s>>>(a);   \
-        } else {                                                     \
-            k_check<DD, MODE, NT, false><<<grid, 256, 0, P.s>>>(a);  \
-        }                                                            \
+#define QR_CASE(DD)                                                                    \
+    case DD:                                                                           \
+        if (ar == kStrict) k_check<DD, MODE, NT, kStrict><<<grid, 256, 0, P.s>>>(a);   \
+        else if (ar == kEps) k_check<DD, MODE, NT, kEps><<<grid, 256, 0, P.s>>>(a);    \
+        else k_check<DD, MODE, NT, kFast><<<grid, 256, 0, P.s>>>(a);                   \
         break;
     bool handled = true;
     QR_DEG_SWITCH(cls.degree, QR_CASE, handled)
 #undef QR_CASE
-    if (!handled) k_check_generic<MODE><<<grid, 256, 0, P.s>>>(a);
+    if (!handled) {
+        if (ar == kStrict) k_check_generic<MODE, kStrict><<<grid, 256, 0, P.s>>>(a);
+        else k_check_generic<MODE, kFast><<<grid, 256, 0, P.s>>>(a);
+    }
     QR_LAUNCH_CHECK();
     return QR_OK;
 }
@@ -534,7 +565,7 @@ static int launch_var(const Plan &P, int f0, int f1) {
 template <int MODE, bool NT>
 static int launch_fused_nt(const Plan &P, const DegreeClass &cls, uint8_t *unsat, int cf0, int cf1, int vf0, int vf1) {
     const CheckArgs ca = P.check_args(cls, P.post, unsat, cf0, cf1);
-    const bool eps = use_eps(MODE);
+    const int ar = math_mode(MODE);
     const VarArgs va = P.var_args(vf0, vf1);
     const unsigned nbc = ca.nbx * (unsigned)((cf1 - cf0) >> ca.g.lft);
     const unsigned nbv = va.nbx * (unsigned)((vf1 - vf0) >> va.g.lft);
@@ -543,11 +574,12 @@ static int launch_fused_nt(const Plan &P, const DegreeClass &cls, uint8_t *unsat
         ProfScope ps(profiling_on() ? std::string("fused_d") + std::to_string(cls.degree) : std::string(), P.s);
 #define QR_CASE(DD)                                                                           \
     case DD:                                                                                  \
-        if (eps) {                                                                            \
-            k_fused_eps<DD, MODE, NT><<<nbc + nbv, 256, 0, P.s>>>(ca, va, nbc, nbc + nbv);   \
-        } else {                                                                              \
-            k_fused<DD, MODE, NT><<<nbc + nbv, 256, 0, P.s>>>(ca, va, nbc, nbc + nbv);       \
-        }                                                                                     \
+        if (ar == kStrict)                                                                    \
+            k_fused<DD, MODE, NT, kStrict><<<nbc + nbv, 256, 0, P.s>>>(ca, va, nbc, nbc + nbv);  \
+        else if (ar == kEps)                                                                  \
+            k_fused<DD, MODE, NT, kEps><<<nbc + nbv, 256, 0, P.s>>>(ca, va, nbc, nbc + nbv);     \
+        else                                                                                  \
+            k_fused<DD, MODE, NT, kFast><<<nbc + nbv, 256, 0, P.s>>>(ca, va, nbc, nbc + nbv);    \
         break;
         QR_DEG_SWITCH(cls.degree, QR_CASE, handled)
 #undef QR_CASE
@@ -701,16 +733,16 @@ __global__ void k_var_nodes(const int64_t *nodes, int64_t n, const int32_t *var_
 }
 
 __global__ void k_check_nodes(const int64_t *nodes, int64_t n, const int32_t *chk_ptr, const int32_t *chk_edge,
-                              const uint8_t *synd, double *c2v, const double *v2c, const MathTables *gtab) {
-    __shared__ MathTables tab;
-    stage_math_tables(&tab, gtab);
+                              const uint8_t *synd, double *c2v, const double *v2c, const GlibcTables *gtab) {
+    __shared__ GlibcTables tab;
+    stage_glibc_tables(&tab, gtab);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int64_t c = nodes[i];
     const int base = chk_ptr[c], d = chk_ptr[c + 1] - base;
     double m[kMaxGenericDeg], out[kMaxGenericDeg];
     for (int k = 0; k < d; ++k) m[k] = v2c[chk_edge[base + k]];
-    check_update_generic(d, m, out, synd[c] ? -1.0 : 1.0, tab);
+    check_update_generic<kStrict>(d, m, out, synd[c] ? -1.0 : 1.0, tab);
     for (int k = 0; k < d; ++k) c2v[chk_edge[base + k]] = out[k];
 }
 
@@ -729,6 +761,7 @@ static int free_code(qr_code *c) {
     (void)hipFree(c->d_var_ptr);
     (void)hipFree(c->d_var_edge);
     (void)hipFree(c->d_mtab);
+    (void)hipFree(c->d_gtab);
     delete c;
     return QR_OK;
 }
@@ -814,7 +847,9 @@ int qr_code_create(const int64_t *e_to_v, const int64_t *e_to_c, int64_t nv, int
     {
         std::vector<MathTables> mt(1);
         build_math_tables(&mt[0]);
-        if ((rc = upload(&code->d_mtab, mt))) {
+        std::vector<GlibcTables> gt(1);
+        build_glibc_tables(&gt[0]);
+        if ((rc = upload(&code->d_mtab, mt)) || (rc = upload(&code->d_gtab, gt))) {
             free_code(code);
             return rc;
         }
@@ -839,7 +874,7 @@ int qr_tune_set(const char *name, int64_t value) {
     std::atomic<int> *k = n == "check_ft" ? &g_tune.check_ft : n == "check_per" ? &g_tune.check_per
                         : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
                         : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
-                        : n == "eps"      ? &g_tune.eps      : n == "eps_max"   ? &g_tune.eps_max
+                        : n == "math"     ? &g_tune.math     : n == "eps_max"   ? &g_tune.eps_max
                         : n == "demap_fast" ? &g_demap_fast : nullptr;
     if (!k) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     if (value < 0 || value > 4096) return set_error(QR_EVALUE, "tuning value out of range");
@@ -852,7 +887,7 @@ int qr_tune_get(const char *name, int64_t *value) {
     const std::atomic<int> *k = n == "check_ft" ? &g_tune.check_ft : n == "check_per" ? &g_tune.check_per
                               : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
                               : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
-                              : n == "eps"      ? &g_tune.eps      : n == "eps_max"   ? &g_tune.eps_max
+                              : n == "math"     ? &g_tune.math     : n == "eps_max"   ? &g_tune.eps_max
                               : n == "demap_fast" ? &g_demap_fast : nullptr;
     if (!k || !value) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     *value = k->load();
@@ -1022,7 +1057,7 @@ int qr_process_check_nodes_host(const qr_code *code, const int64_t *nodes, int64
     QR_HIP(hipMemcpy(d_c2v, c2v, E * 8, hipMemcpyHostToDevice));
     QR_HIP(hipMemcpy(d_v2c, v2c, E * 8, hipMemcpyHostToDevice));
     k_check_nodes<<<(unsigned)((n + 255) / 256), 256>>>(d_nodes, n, code->d_chk_ptr, code->d_chk_edge, d_synd, d_c2v,
-                                                        d_v2c, code->d_mtab);
+                                                        d_v2c, code->d_gtab);
     QR_LAUNCH_CHECK();
     QR_HIP(hipMemcpy(c2v, d_c2v, E * 8, hipMemcpyDeviceToHost));
     return QR_OK;

@@ -1,0 +1,256 @@
+// glibc_math.hpp -- bit-exact restatement of the host libm's exp() and log() for the
+// strict box-plus (decoder.pyx:41-45 evaluated exactly as the reference evaluates it).
+//
+// The reference computes h(t) = log(1.0 + exp(-t)) with glibc.  On x86-64 with FMA
+// (every host of this project: the EPYC GPU-box hosts and the build container),
+// glibc 2.35 resolves exp/log to __exp_fma / __log_fma: sysdeps/ieee754/dbl-64/e_exp.c
+// and e_log.c (the ARM optimized-routines algorithms) compiled with -mfma, i.e. with
+// GCC's floating-point contraction.  The functions below repeat those routines
+// operation for operation -- every fma exactly where the compiled routine has a
+// vfmadd/vfnmadd, every other operation as a separately rounded IEEE op -- so that
+// on any IEEE fp64 machine (gfx950 VALU included) they return the same bits.  The
+// data (128-entry tables and coefficients) is extracted from the library itself at
+// build time (gen_glibc_tables.py -> build/glibc_tables.inc).
+//
+//   exp(x), x in [-512, 512], |x| >= 2^-54 (abstop in range, e_exp.c:90-140):
+//     kd = fma(x, InvLn2N, Shift); ki = bits(kd); kd -= Shift
+//     r  = fma(kd, NegLn2loN, fma(kd, NegLn2hiN, x))
+//     tail, sbits = T[ki % 128] (+ ki << 45)
+//     tmp = fma(r^4, fma(r, C5, C4), fma(fma(r, C3, C2), r^2, tail + r))
+//     exp = fma(scale, tmp, scale)
+//   |x| < 2^-54: 1.0 + x.
+//
+//   log(x), x positive normal (e_log.c:40-140):
+//     x in [1 - 2^-4, 1 + 0x1.09p-4): the near-1 polynomial of degree 12 with the
+//       hi/lo split of r = x - 1 (see g_log below for the contraction pattern);
+//     otherwise: i, k from the top bits of x - OFF, r = fma(z, invc_i, -1),
+//       w = fma(k, Ln2hi, logc_i), hi = r + w, lo = fma(k, Ln2lo, (w - hi) + r),
+//       log = fma(r^3, fma(fma(r, A4, A3), r^2, fma(r, A2, A1)), fma(r^2, A0, lo)) + hi.
+//
+// tests/test_glibc_math.py runs these on the host against libm's exp/log on ~10^7
+// inputs (dense on the box-plus domain) and requires identical bits; the GPU tests
+// then require decodes bit-identical to the oracle (which calls libm).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "glibc_tables.inc"
+
+namespace qr {
+
+// {tail, sbits} per exp interval and {invc, logc} per log interval: 4 KiB, staged in LDS.
+struct GlibcTables {
+    double2 ex[128];
+    double2 lg[128];
+};
+
+inline void build_glibc_tables(GlibcTables *t) {
+    for (int i = 0; i < 128; ++i) {
+        t->ex[i].x = __builtin_bit_cast(double, kGxTab[2 * i]);
+        t->ex[i].y = __builtin_bit_cast(double, kGxTab[2 * i + 1]);
+        t->lg[i].x = kGlTab[2 * i];
+        t->lg[i].y = kGlTab[2 * i + 1];
+    }
+}
+
+__device__ __forceinline__ void stage_glibc_tables(GlibcTables *lds, const GlibcTables *__restrict__ g) {
+    const double2 *src = reinterpret_cast<const double2 *>(g);
+    double2 *dst = reinterpret_cast<double2 *>(lds);
+    constexpr int n = sizeof(GlibcTables) / sizeof(double2);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+}
+
+__host__ __device__ __forceinline__ uint32_t g_hi(double x) { return (uint32_t)(__builtin_bit_cast(uint64_t, x) >> 32); }
+__host__ __device__ __forceinline__ uint32_t g_lo(double x) { return (uint32_t)__builtin_bit_cast(uint64_t, x); }
+__host__ __device__ __forceinline__ double g_make(uint32_t hi, uint32_t lo) {
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// glibc exp(x) for |x| < 512 (finite; NaN propagates).  The table index and the
+// exponent come from the low word of kd (|ki| < 2^17, so ki << 45 only touches the
+// high word of sbits).
+__host__ __device__ __forceinline__ double g_exp(double x, const GlibcTables &T) {
+    double kd = __builtin_fma(x, kGxInvLn2N, kGxShift);
+    const uint32_t ki = g_lo(kd);
+    kd = kd - kGxShift;
+    double r = __builtin_fma(kd, kGxNegLn2hiN, x);
+    r = __builtin_fma(kd, kGxNegLn2loN, r);
+    const double2 e = T.ex[ki & 127u];
+    const double scale = g_make(g_hi(e.y) + (ki << 13), g_lo(e.y));  // sbits = T[2i+1] + (ki << 45)
+    const double r2 = r * r;
+    const double p23 = __builtin_fma(r, kGxC3, kGxC2);
+    const double tr = e.x + r;
+    const double p45 = __builtin_fma(r, kGxC5, kGxC4);
+    const double a = __builtin_fma(p23, r2, tr);
+    const double r4 = r2 * r2;
+    const double tmp = __builtin_fma(r4, p45, a);
+    const double res = __builtin_fma(scale, tmp, scale);
+    return (__builtin_fabs(x) < 0x1p-54) ? 1.0 + x : res;
+}
+
+// glibc log(x) for positive normal finite x (the box-plus only needs x in [1, 2]).
+__host__ __device__ __forceinline__ double g_log(double x, const GlibcTables &T) {
+    const uint32_t hx = g_hi(x);
+    double y;
+    if (hx - 0x3FEE0000u < 0x3FF10900u - 0x3FEE0000u) {
+        // x in [1 - 2^-4, 1 + 0x1.09p-4): e_log.c "close to 1.0" branch
+        const double r = x - 1.0;
+        double p2 = __builtin_fma(r, kGlB2, kGlB1);
+        double p5 = __builtin_fma(r, kGlB5, kGlB4);
+        const double r2 = r * r;
+        double p8 = __builtin_fma(r, kGlB8, kGlB7);
+        p2 = __builtin_fma(r2, kGlB3, p2);
+        p5 = __builtin_fma(r2, kGlB6, p5);
+        const double r3 = r * r2;
+        p8 = __builtin_fma(r2, kGlB9, p8);
+        p8 = __builtin_fma(r3, kGlB10, p8);
+        p5 = __builtin_fma(p8, r3, p5);
+        const double P = __builtin_fma(p5, r3, p2);
+        // rhi = r + w - w, w = r * 2^27 (contracted: both steps are fmas)
+        const double t = __builtin_fma(r, 0x1p27, r);
+        const double rhi = __builtin_fma(-0x1p27, r, t);
+        const double rhi2 = rhi * rhi;
+        const double rlo = r - rhi;
+        const double hi = __builtin_fma(rhi2, kGlB0, r);    // r + rhi*rhi*B0
+        const double d = r - hi;
+        const double rr = r + rhi;
+        double lo = __builtin_fma(rhi2, kGlB0, d);          // r - hi + w
+        const double q = kGlB0 * rlo;
+        lo = __builtin_fma(q, rr, lo);                      // lo += B0*rlo*(rhi + r)
+        const double yy = __builtin_fma(P, r3, lo);         // y = r3*P; y += lo
+        y = hi + yy;                                        // y += hi
+        if (__builtin_bit_cast(uint64_t, x) == 0x3FF0000000000000ull) y = 0.0;
+    } else {
+        // OFF = 0x3fe6000000000000: only the high word takes part in the index arithmetic
+        const uint32_t th = hx - 0x3FE60000u;
+        const uint32_t i = (th >> 13) & 127u;
+        const int k = (int)th >> 20;
+        const double z = g_make(hx - (th & 0xFFF00000u), g_lo(x));
+        const double2 c = T.lg[i];                          // {invc, logc}
+        const double r = __builtin_fma(z, c.x, -1.0);
+        const double kd = (double)k;
+        const double w = __builtin_fma(kd, kGlLn2hi, c.y);
+        const double pA = __builtin_fma(r, kGlA2, kGlA1);
+        const double hi = r + w;
+        const double r2 = r * r;
+        double lo = w - hi;
+        lo = lo + r;
+        lo = __builtin_fma(kd, kGlLn2lo, lo);
+        const double r3 = r * r2;
+        double pB = __builtin_fma(r, kGlA4, kGlA3);
+        lo = __builtin_fma(r2, kGlA0, lo);
+        pB = __builtin_fma(pB, r2, pA);
+        y = __builtin_fma(r3, pB, lo) + hi;
+    }
+    return y;
+}
+
+// ---- the box-plus domain: h(t) = log(1.0 + exp(-t)), t >= 0, inf or NaN ----------------
+//
+// exp(x) for x in [-37.51, 0] or NaN: g_exp without the |x| < 2^-54 case, which the
+// main path already rounds to exactly 1.0 + x there (= 1.0; tests/native pin it).
+__host__ __device__ __forceinline__ double g_exp_neg(double x, const GlibcTables &T) {
+    double kd = __builtin_fma(x, kGxInvLn2N, kGxShift);
+    const uint32_t ki = g_lo(kd);
+    kd = kd - kGxShift;
+    double r = __builtin_fma(kd, kGxNegLn2hiN, x);
+    r = __builtin_fma(kd, kGxNegLn2loN, r);
+    const double2 e = T.ex[ki & 127u];
+    const double scale = g_make(g_hi(e.y) + (ki << 13), g_lo(e.y));
+    const double r2 = r * r;
+    const double p23 = __builtin_fma(r, kGxC3, kGxC2);
+    const double tr = e.x + r;
+    const double p45 = __builtin_fma(r, kGxC5, kGxC4);
+    const double a = __builtin_fma(p23, r2, tr);
+    const double r4 = r2 * r2;
+    const double tmp = __builtin_fma(r4, p45, a);
+    return __builtin_fma(scale, tmp, scale);
+}
+
+// log(u) for u = 1.0 + exp(-t) in [1, 2] or NaN: g_log with the main path's scaled
+// mantissa z = u 2^-k taken by ldexp (exact; it also carries a NaN through, which
+// the bit arithmetic would not), and without the u == 1 early return (both branches
+// return +0 there).
+__host__ __device__ __forceinline__ double g_log_u(double x, const GlibcTables &T) {
+    const uint32_t hx = g_hi(x);
+    if (hx < 0x3FF10900u) {  // u in [1, 1 + 0x1.09p-4): the near-1 branch
+        const double r = x - 1.0;
+        double p2 = __builtin_fma(r, kGlB2, kGlB1);
+        double p5 = __builtin_fma(r, kGlB5, kGlB4);
+        const double r2 = r * r;
+        double p8 = __builtin_fma(r, kGlB8, kGlB7);
+        p2 = __builtin_fma(r2, kGlB3, p2);
+        p5 = __builtin_fma(r2, kGlB6, p5);
+        const double r3 = r * r2;
+        p8 = __builtin_fma(r2, kGlB9, p8);
+        p8 = __builtin_fma(r3, kGlB10, p8);
+        p5 = __builtin_fma(p8, r3, p5);
+        const double P = __builtin_fma(p5, r3, p2);
+        const double t = __builtin_fma(r, 0x1p27, r);
+        const double rhi = __builtin_fma(-0x1p27, r, t);
+        const double rhi2 = rhi * rhi;
+        const double rlo = r - rhi;
+        const double hi = __builtin_fma(rhi2, kGlB0, r);
+        const double d = r - hi;
+        const double rr = r + rhi;
+        double lo = __builtin_fma(rhi2, kGlB0, d);
+        const double q = kGlB0 * rlo;
+        lo = __builtin_fma(q, rr, lo);
+        return hi + __builtin_fma(P, r3, lo);
+    }
+    const uint32_t th = hx - 0x3FE60000u;
+    const int k = (int)th >> 20;
+    const double2 c = T.lg[(th >> 13) & 127u];
+    const double z = __builtin_ldexp(x, -k);
+    const double r = __builtin_fma(z, c.x, -1.0);
+    const double kd = (double)k;
+    const double w = __builtin_fma(kd, kGlLn2hi, c.y);
+    const double pA = __builtin_fma(r, kGlA2, kGlA1);
+    const double hi = r + w;
+    const double r2 = r * r;
+    double lo = w - hi;
+    lo = lo + r;
+    lo = __builtin_fma(kd, kGlLn2lo, lo);
+    const double r3 = r * r2;
+    double pB = __builtin_fma(r, kGlA4, kGlA3);
+    lo = __builtin_fma(r2, kGlA0, lo);
+    pB = __builtin_fma(pB, r2, pA);
+    return __builtin_fma(r3, pB, lo) + hi;
+}
+
+// h(t) exactly as the reference evaluates it.  t > 37.5 is moved into
+// [37.5, 37.5 + 2^-15) by replacing its high word (there exp(-t) < 2^-54, so
+// 1.0 + exp(-t) == 1.0 and log(1.0) == 0, exactly what the reference returns for
+// every t >= 36.74, inf included); NaN fails the compare and propagates.
+__host__ __device__ __forceinline__ double h_strict(double t, const GlibcTables &T) {
+    const double tc = g_make((t > 37.5) ? 0x4042C000u : g_hi(t), g_lo(t));
+    return g_log_u(1.0 + g_exp_neg(-tc, T), T);
+}
+
+// decoder.pyx:41-45: (sgn(a)sgn(b) * min + h(|a+b|)) - h(|a-b|), each operation
+// rounded separately.  sgn(a)sgn(b)*min == copysign(min, a*b) up to the sign of an
+// exact zero and NaN cases, neither of which changes the result (fastmath.hpp).
+// QR_STRICT_MAXMIN: the two h are taken at t+ = |a|+|b| and t- = ||a|-|b|| (the same
+// two values: |a+b| = t+ and |a-b| = t- when a*b >= 0, swapped otherwise, exactly, also
+// for zeros, infinities and NaN) so that each call site sees one population (t+ mostly
+// beyond the near-1 threshold t = 2.738 of g_log, t- mostly below) and its waves
+// rarely have to run both branches of g_log.
+#ifndef QR_STRICT_MAXMIN
+#define QR_STRICT_MAXMIN 1
+#endif
+__host__ __device__ __forceinline__ double box_plus_strict(double a, double b, const GlibcTables &T) {
+    const double m = fmin(fabs(a), fabs(b));
+    const double ab = a * b;
+    const double sm = copysign(m, ab);
+#if QR_STRICT_MAXMIN
+    const double hp = h_strict(fabs(a) + fabs(b), T);
+    const double hm = h_strict(fabs(fabs(a) - fabs(b)), T);
+    const bool same = !(ab < 0.0);
+    return (sm + (same ? hp : hm)) - (same ? hm : hp);
+#else
+    return (sm + h_strict(fabs(a + b), T)) - h_strict(fabs(a - b), T);
+#endif
+}
+
+}  // namespace qr

@@ -11,6 +11,7 @@
 #include "qamr.h"
 #include "qamr_math.hpp"
 #include "fastmath.hpp"
+#include "glibc_math.hpp"
 
 namespace qr {
 
@@ -91,6 +92,7 @@ struct qr_code {
     int32_t *d_var_ptr = nullptr, *d_var_edge = nullptr;
     std::vector<DegreeClass> classes;
     qr::MathTables *d_mtab = nullptr;  // box-plus exp/log tables (fastmath.hpp)
+    qr::GlibcTables *d_gtab = nullptr; // strict box-plus: glibc exp/log data (glibc_math.hpp)
     mutable qr::Scratch scratch;
 };
 

@@ -4,7 +4,7 @@
 
 For each (PAM order, SNR) operating point: B frames generated on the GPU by the
 softening pipeline, decoded by the oracle (reference arithmetic, CPU) and by
-libqamr with eps=0 (exact box-plus) and eps=1 at several eps_max.  Prints
+libqamr with math=0 (strict, glibc-exact), 1 (table h) and 2 (exp domain) at several eps_max.  Prints
 success/iteration/hard-decision agreement, the worst LAPPR error in units of the
 north-star tolerance (1e-6 |ref| + 1e-9), and the share of lanes of the
 checks' input magnitudes above each eps_max (from the oracle's final LAPPRs).
@@ -52,18 +52,18 @@ def main():
               f"|lappr| p50/p99/max {np.percentile(np.abs(llr), 50):.1f}/{np.percentile(np.abs(llr), 99):.1f}/"
               f"{np.abs(llr).max():.1f}, |final| p50/p99 {np.percentile(np.abs(f2[fin]), 50):.1f}/"
               f"{np.percentile(np.abs(f2[fin]), 99):.1f}", flush=True)
-        runs = [(0, 40)] + [(1, int(e)) for e in args.eps_max.split(",")]
+        runs = [(0, 40), (1, 40)] + [(2, int(e)) for e in args.eps_max.split(",")]
         for eps, emax in runs:
-            _lib.tune_set("eps", eps)
+            _lib.tune_set("math", eps)
             _lib.tune_set("eps_max", emax)
             s1, i1, f1 = dec.decode_batch(llr, synd, 50)
             m = np.isfinite(f2) & np.isfinite(f1)
             ratio = np.abs(f1[m] - f2[m]) / (1e-6 * np.abs(f2[m]) + 1e-9)
-            print(f"  eps={eps} eps_max={emax:4d}: success eq {np.array_equal(s1, s2)}, iters eq "
+            print(f"  math={eps} eps_max={emax:4d}: success eq {np.array_equal(s1, s2)}, iters eq "
                   f"{np.array_equal(i1, i2)}, hard eq {np.array_equal(f1 < 0, f2 < 0)}, nan eq "
                   f"{np.array_equal(np.isnan(f1), np.isnan(f2))}, worst err/tol {ratio.max():.3g}, "
                   f"n over tol {(ratio > 1).sum()}, bit-identical share {(f1[m] == f2[m]).mean():.4f}", flush=True)
-        _lib.tune_set("eps", 1)
+        _lib.tune_set("math", 0)
         _lib.tune_set("eps_max", 40)
 
 

@@ -14,7 +14,7 @@ for v in "${VS[@]}"; do
 import csv, glob, sys
 d, v = sys.argv[1], sys.argv[2]
 f = [float(r["Counter_Value"]) for p in glob.glob(d + "/**/run_counter_collection.csv", recursive=True)
-     for r in csv.DictReader(open(p)) if r["Kernel_Name"].startswith("void qr::k_fused_eps<7, 1")]
+     for r in csv.DictReader(open(p)) if r["Kernel_Name"].startswith("void qr::k_fused<7, 1, true, 0")]
 print(v, "fused launches", len(f), "FETCH GB/launch (x2)", round(2 * sum(f) / len(f) * 1024 / 1e9, 3) if f else None)
 PY
 done

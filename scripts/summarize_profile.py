@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise a scripts/profile_session.sh output directory.
 
-    python scripts/summarize_profile.py gpurun_out/prof_r1 [--kernel k_fused_eps<7, 1, true>]
+    python scripts/summarize_profile.py gpurun_out/prof_r1 [--kernel 'k_fused<7, 1, true, 0>'] [--math 0]
 
 Writes <dir>/summary.md (per-kernel time from --kernel-trace --stats, PMC counters
 per launch) and <dir>/pmc_traffic.json: HBM bytes per launch of the dominant
@@ -25,7 +25,8 @@ def short(name):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--kernel", default="k_fused_eps<7, 1, true>")
+    ap.add_argument("--kernel", default="k_fused<7, 1, true, 0>")
+    ap.add_argument("--math", type=int, default=0, help="decoder arithmetic (knob math) of the profiled run")
     ap.add_argument("--kernel-key", default="fused_d7")
     ap.add_argument("--workload", default="dvbs2_4pam")
     ap.add_argument("--batch", type=int, default=4096)
@@ -59,6 +60,7 @@ def main():
         fetch = sum(kc["FETCH_SIZE"]) / len(kc["FETCH_SIZE"])
         write = sum(kc["WRITE_SIZE"]) / len(kc["WRITE_SIZE"])
         out = {"workload": args.workload, "batch": args.batch, "kernel": args.kernel, "kernel_key": args.kernel_key,
+               "math": args.math,
                "fetch_size_kib": fetch, "write_size_kib": write,
                "hbm_bytes_per_launch": int((2 * fetch + write) * 1024),
                "correction": "2*FETCH_SIZE + WRITE_SIZE, KiB -> bytes (MI355X_MICROARCH.md HBM section)",

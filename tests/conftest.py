@@ -53,3 +53,20 @@ def assert_llr_close(got, ref, rtol=LLR_RTOL, atol=LLR_ATOL):
     lim = rtol * np.abs(ref[m]) + atol
     bad = err > lim
     assert not bad.any(), f"{bad.sum()} LAPPRs out of tolerance; worst |d|={err.max():.3e}"
+
+
+def assert_bit_exact(got, ref):
+    """Identical doubles (signed zeros included); NaN matches NaN whatever its payload.
+    The decoder's default arithmetic (knob math = 0, glibc_math.hpp) reproduces the
+    reference's exp/log, so its outputs must equal the reference's bit for bit."""
+    got = np.ascontiguousarray(got, np.float64)
+    ref = np.ascontiguousarray(ref, np.float64)
+    assert got.shape == ref.shape
+    nan_g, nan_r = np.isnan(got), np.isnan(ref)
+    assert np.array_equal(nan_g, nan_r), f"NaN pattern differs ({nan_g.sum()} vs {nan_r.sum()})"
+    m = ~nan_r
+    diff = got[m].view(np.int64) != ref[m].view(np.int64)
+    if diff.any():
+        k = np.flatnonzero(diff)[0]
+        raise AssertionError(f"{diff.sum()} of {m.sum()} values differ; first: got {got[m][k]!r} ref {ref[m][k]!r} "
+                             f"(|d| = {abs(got[m][k] - ref[m][k]):.3e})")

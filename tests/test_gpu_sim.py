@@ -5,7 +5,7 @@ import ctypes as C
 import numpy as np
 import pytest
 
-from conftest import assert_llr_close, golden
+from conftest import assert_bit_exact, assert_llr_close, golden
 
 import oracle as O
 
@@ -81,8 +81,7 @@ def test_simulator_batch_vs_oracle(gpu, mode):
     s2, i2, f2 = orc.decode_batch(L, Sy, 30)
     assert np.array_equal(succ.cpu().numpy(), s2) and np.array_equal(its.cpu().numpy(), i2)
     F1 = fin[:, :96].cpu().numpy().T
-    assert np.array_equal(F1 < 0, f2 < 0)
-    assert_llr_close(F1, f2)
+    assert_bit_exact(F1, f2)
 
 
 def test_run_snr_and_cli(gpu, tmp_path):
