@@ -297,7 +297,9 @@ __global__ void __launch_bounds__(256) k_var(VarArgs a) {
 //     3.14 (5 waves) / 3.26 (4 waves);
 //   exp domain (QR_FUSED_EPS_WAVES, 5 waves = 96 VGPRs, no spill): 2.73 ms vs 3.21
 //     (6 waves, 80 B spilled per lane inside the loop) / 2.94 (4 waves).
-//   strict box-plus (QR_FUSED_STRICT_WAVES): to be tuned.
+//   strict box-plus (QR_FUSED_STRICT_WAVES, 4 waves = 128 VGPRs): 5.56 ms vs 5.68 (5
+//     waves, 96 VGPRs); issue-bound on fp64 VALU (the F and B chains evaluated side by
+//     side for more ILP: no gain).
 #ifndef QR_FUSED_WAVES
 #define QR_FUSED_WAVES 6
 #endif
@@ -305,7 +307,7 @@ __global__ void __launch_bounds__(256) k_var(VarArgs a) {
 #define QR_FUSED_EPS_WAVES 5
 #endif
 #ifndef QR_FUSED_STRICT_WAVES
-#define QR_FUSED_STRICT_WAVES 5
+#define QR_FUSED_STRICT_WAVES 4
 #endif
 template <int AR>
 struct FusedWaves {

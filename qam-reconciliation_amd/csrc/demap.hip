@@ -30,7 +30,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QR_DEM
                                                const int64_t *__restrict__ j, double alpha,
                                                double *__restrict__ lappr) {
     __shared__ MathTables mt;
+    __shared__ GlibcTables gt;
     stage_math_tables(&mt, gmt);
+    stage_glibc_tables(&gt, &kGlibcConst);
     const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t s = item / ld;
     const int f = (int)(item - s * ld);
@@ -43,7 +45,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QR_DEM
 #pragma unroll
         for (int k = 0; k < BPS; ++k) out[k] = __builtin_nan("");
     } else {
-        demap_symbol<FAST, BPS>(t, mt, nv, (int)jv, alpha, out);
+        demap_symbol<FAST, BPS>(t, mt, gt, nv, (int)jv, alpha, out);
     }
 #pragma unroll
     for (int k = 0; k < BPS; ++k) lappr[(s * BPS + k) * ld + f] = out[k];
@@ -109,7 +111,7 @@ __global__ void __launch_bounds__(256) k_direct_lappr(const DemapTables *__restr
     for (int k = 0; k < kMaxBps; ++k) { N[k] = 0; D[k] = 0; }
     for (int i = 0; i < t.M; ++i) {
         const double d = yv - t.a[i];
-        const double add = exp(-(d * d) / two_var);
+        const double add = g_exp_full(-(d * d) / two_var, kGlibcConst);
         int mi = i;
 #pragma unroll
         for (int k = 0; k < kMaxBps; ++k) {
@@ -122,7 +124,7 @@ __global__ void __launch_bounds__(256) k_direct_lappr(const DemapTables *__restr
     }
 #pragma unroll
     for (int k = 0; k < kMaxBps; ++k)
-        if (k < t.bps) lappr[(s * t.bps + k) * ld + f] = log(N[k]) - log(D[k]);
+        if (k < t.bps) lappr[(s * t.bps + k) * ld + f] = g_log_full(N[k], kGlibcConst) - g_log_full(D[k], kGlibcConst);
 }
 
 // Hard reverse reconciliation (noisemapper.pyx:423-432, bare_llr): Alice's LAPPRs
@@ -285,7 +287,6 @@ int qr_demap_create(int32_t bps, const double *constellation, const double *prob
     for (int i = 1; i < M; ++i) t.Fthr[i] = single_F_Y(t, t.thr[i]);
     for (int i = 0; i < M; ++i) t.dF[i] = t.Fthr[i + 1] - t.Fthr[i];  // :159-162
     t.inv_den = 1.0 / t.den;
-    t.inv_two_s2 = 1.0 / t.two_s2;
     t.amin = t.amax = t.a[0];
     for (int i = 1; i < M; ++i) { t.amin = fmin(t.amin, t.a[i]); t.amax = fmax(t.amax, t.a[i]); }
     // Newton start table (qamr_math.hpp, build_quantiles): M * kQStride * M exact F_Y

@@ -146,6 +146,97 @@ __host__ __device__ __forceinline__ double g_log(double x, const GlibcTables &T)
     return y;
 }
 
+// ---- full-range exp / log (the demapper: noisemapper.pyx:503-515, 534; erfc's exp) --------
+//
+// __exp_fma for every input: |x| < 2^-54 -> 1.0 + x; |x| >= 1024, inf, NaN -> 0, 1.0 + x
+// (inf/NaN) or the overflow/underflow result; 512 <= |x| < 1024 -> the main path with the
+// e_exp.c specialcase() rescaling (contraction pattern of the compiled routine: k > 0
+// fuses scale + scale*tmp, k < 0 does not, it reuses scale*tmp).
+__host__ __device__ __forceinline__ double g_exp_full(double x, const GlibcTables &T) {
+    const uint32_t abstop = (g_hi(x) >> 20) & 0x7FFu;
+    if (abstop - 0x3C9u >= 0x3Fu) {
+        if ((int)(abstop - 0x3C9u) < 0) return 1.0 + x;
+        if (abstop >= 0x409u) {
+            if (__builtin_bit_cast(uint64_t, x) == 0xFFF0000000000000ull) return 0.0;
+            if (abstop >= 0x7FFu) return 1.0 + x;
+            return (g_hi(x) >> 31) ? 0.0 : __builtin_inf();
+        }
+    }
+    double kd = __builtin_fma(x, kGxInvLn2N, kGxShift);
+    const uint32_t ki = g_lo(kd);
+    kd = kd - kGxShift;
+    double r = __builtin_fma(kd, kGxNegLn2hiN, x);
+    r = __builtin_fma(kd, kGxNegLn2loN, r);
+    const double2 e = T.ex[ki & 127u];
+    const uint32_t shi = g_hi(e.y) + (ki << 13), slo = g_lo(e.y);
+    const double r2 = r * r;
+    const double p23 = __builtin_fma(r, kGxC3, kGxC2);
+    const double tr = e.x + r;
+    const double p45 = __builtin_fma(r, kGxC5, kGxC4);
+    const double a = __builtin_fma(p23, r2, tr);
+    const double r4 = r2 * r2;
+    const double tmp = __builtin_fma(r4, p45, a);
+    if (abstop < 0x408u) {  // the common case: no rescaling
+        const double scale = g_make(shi, slo);
+        return __builtin_fma(scale, tmp, scale);
+    }
+    if (!(ki & 0x80000000u)) {  // k > 0: sbits -= 1009 << 52
+        const double scale = g_make(shi - 0x3F100000u, slo);
+        return __builtin_fma(scale, tmp, scale) * 0x1p1009;
+    }
+    const double scale = g_make(shi + 0x3FE00000u, slo);  // k < 0: sbits += 1022 << 52
+    const double st = scale * tmp;
+    double y = scale + st;
+    if (y < 1.0) {
+        const double hi = y + 1.0;
+        const double lo = (scale - y) + st;
+        double t = (1.0 - hi) + y;
+        t = t + lo;
+        t = t + hi;
+        y = t - 1.0;
+        if (y == 0.0) y = 0.0;
+    }
+    return y * 0x1p-1022;
+}
+
+// __log_fma for every input: 0 -> -inf, +inf -> +inf, negative or NaN -> NaN, subnormals
+// rescaled by 2^52 into the main path (e_log.c special cases).
+__host__ __device__ __forceinline__ double g_log_full(double x, const GlibcTables &T) {
+    uint32_t hx = g_hi(x), lx = g_lo(x);
+    if (hx - 0x3FEE0000u < 0x3FF10900u - 0x3FEE0000u) return g_log(x, T);
+    const uint32_t top = hx >> 16;
+    if (top - 0x0010u >= 0x7FF0u - 0x0010u) {
+        if ((hx << 1) == 0 && lx == 0) return -__builtin_inf();
+        if (hx == 0x7FF00000u && lx == 0) return x;
+        if ((top & 0x8000u) || (top & 0x7FF0u) == 0x7FF0u) return __builtin_nan("");
+        const double xs = x * 0x1p52;  // subnormal: ix = asuint64(x * 2^52) - (52 << 52)
+        hx = g_hi(xs) - (52u << 20);
+        lx = g_lo(xs);
+    }
+    const uint32_t th = hx - 0x3FE60000u;
+    const int k = (int)th >> 20;
+    const double2 c = T.lg[(th >> 13) & 127u];
+    const double z = g_make(hx - (th & 0xFFF00000u), lx);
+    const double r = __builtin_fma(z, c.x, -1.0);
+    const double kd = (double)k;
+    const double w = __builtin_fma(kd, kGlLn2hi, c.y);
+    const double pA = __builtin_fma(r, kGlA2, kGlA1);
+    const double hi = r + w;
+    const double r2 = r * r;
+    double lo = w - hi;
+    lo = lo + r;
+    lo = __builtin_fma(kd, kGlLn2lo, lo);
+    const double r3 = r * r2;
+    double pB = __builtin_fma(r, kGlA4, kGlA3);
+    lo = __builtin_fma(r2, kGlA0, lo);
+    pB = __builtin_fma(pB, r2, pA);
+    return __builtin_fma(r3, pB, lo) + hi;
+}
+
+// The tables as device constant data, for call sites that have no LDS copy at hand
+// (the rare erfc exp of the demapper's exact F_Y evaluations).
+__constant__ static const GlibcTables kGlibcConst = QR_GLIBC_TABLES_INIT;
+
 // ---- the box-plus domain: h(t) = log(1.0 + exp(-t)), t >= 0, inf or NaN ----------------
 //
 // exp(x) for x in [-37.51, 0] or NaN: g_exp without the |x| < 2^-54 case, which the

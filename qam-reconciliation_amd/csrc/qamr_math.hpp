@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "fastmath.hpp"
+#include "glibc_math.hpp"
 
 #define QR_HD __host__ __device__ __forceinline__
 
@@ -60,7 +61,11 @@ struct CephesErf {
 QR_HD double erfc_ge1(double x) {
     double z = -x * x;
     if (z < -CephesErf::MAXLOG) return 0.0;
+#ifdef __HIP_DEVICE_COMPILE__
+    z = g_exp_full(z, kGlibcConst);  // glibc's exp, bit for bit (glibc_math.hpp)
+#else
     z = exp(z);
+#endif
     double p, q;
     if (x < 8.0) {
         p = CephesErf::P[0];
@@ -117,7 +122,6 @@ struct DemapTables {
     double dF[kMaxOrder];       // delta_F_Y
     uint8_t sign[kMaxOrder];    // sign_config
     double inv_den;             // 1 / den (Newton only)
-    double inv_two_s2;          // 1 / two_s2
     double amin, amax;          // constellation extremes (Newton window bound)
     // Piecewise Taylor table of F_Y (Newton only, see build_ftab): interval j covers
     // [lo + j w, lo + (j+1) w]; kFtabDeg+1 coefficients in t = 2 (y - lo)/w - 2j - 1.
@@ -572,8 +576,11 @@ inline void build_quantiles(const DemapTables &t, double2 *quant) {
 // Note the reference quirk kept on purpose: no /2sigma^2 for k < j (:503-507).
 // BPS (= t.bps) is a template parameter: exact-size accumulators (fewer VGPRs, higher
 // occupancy) and compile-time trip counts for the M = 2^BPS hypothesis / LLR loops.
+// The exp of the LLR sums and the final log are glibc's, restated bit for bit
+// (glibc_math.hpp, tables `gt` in LDS): the LAPPRs equal the reference's bit for bit.
 template <bool FAST, int BPS>
-QR_HD void demap_symbol(const DemapTables& t, const MathTables& mt, double n, int j, double alpha, double* out) {
+QR_HD void demap_symbol(const DemapTables& t, const MathTables& mt, const GlibcTables& gt, double n, int j, double alpha,
+                        double* out) {
     constexpr int M = 1 << BPS;
     double N[BPS], D[BPS];
 #pragma unroll
@@ -588,11 +595,11 @@ QR_HD void demap_symbol(const DemapTables& t, const MathTables& mt, double n, in
 #endif
         double s = 0;
 #ifndef QR_EXPERIMENT_NO_LLR
-        for (int k = 0; k < j; ++k) s += exp_fast((2 * y - t.a[k] - aj) * (t.a[k] - aj), mt) * t.p[k];
+        for (int k = 0; k < j; ++k) s += g_exp_full((2 * y - t.a[k] - aj) * (t.a[k] - aj), gt) * t.p[k];
 #endif
         s += t.p[j];
 #ifndef QR_EXPERIMENT_NO_LLR
-        for (int k = j + 1; k < M; ++k) s += exp_fast((2 * y - t.a[k] - aj) * (t.a[k] - aj) * t.inv_two_s2, mt) * t.p[k];
+        for (int k = j + 1; k < M; ++k) s += g_exp_full((2 * y - t.a[k] - aj) * (t.a[k] - aj) / t.two_s2, gt) * t.p[k];  // a division, as :512-515
 #else
         s += y * 1e-300;
 #endif
@@ -607,7 +614,7 @@ QR_HD void demap_symbol(const DemapTables& t, const MathTables& mt, double n, in
     }
     // reconciliation.pyx:144-145 (lappr *= alpha) fused into the store.
 #pragma unroll
-    for (int k = 0; k < BPS; ++k) out[k] = (log(N[k]) - log(D[k])) * alpha;
+    for (int k = 0; k < BPS; ++k) out[k] = (g_log_full(N[k], gt) - g_log_full(D[k], gt)) * alpha;
 }
 
 // noisemapper.pyx:27-44 (__binsearch over the M+1 thresholds), iterative.

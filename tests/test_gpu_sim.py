@@ -41,7 +41,7 @@ def test_direct_and_bare_llr_vs_reference(gpu, key, bps):
     _lib.check(_lib.load().qr_direct_lappr_device(nm.handle, two_var, 1, 64, S, C.c_void_p(yt.data_ptr()),
                                                   C.c_void_p(out.data_ptr()), None))
     torch.cuda.synchronize()
-    assert_llr_close(out[:, 0].cpu().numpy(), g[f"{key}_direct"])
+    assert_bit_exact(out[:, 0].cpu().numpy(), g[f"{key}_direct"])
     # bare-LLR table lookup: bit-exact (host table is bit-exact, lookup is a copy)
     x = g[f"{key}_x"]
     xt = _col(x, dtype=torch.int64)
