@@ -41,15 +41,24 @@ enum CheckMode { kFirst = 0, kNormal = 1, kParityOnly = 2 };
 //              eps_max take the kFast box-plus).
 enum MathMode { kStrict = 0, kFast = 1, kEps = 2 };
 
+// Tab: the tables staged in LDS; Regs: per-thread constants kept in VGPRs.
 template <int AR>
 struct Arith {  // kFast, kEps: MathTables (10 KiB) in LDS
     using Tab = MathTables;
-    static __device__ __forceinline__ double bp(double a, double b, const Tab &T) { return box_plus_fast(a, b, T); }
+    struct Regs {};
+    static __device__ __forceinline__ Regs regs() { return Regs{}; }
+    static __device__ __forceinline__ double bp(double a, double b, const Tab &T, const Regs &) {
+        return box_plus_fast(a, b, T);
+    }
 };
 template <>
 struct Arith<kStrict> {  // GlibcTables (4 KiB) in LDS
     using Tab = GlibcTables;
-    static __device__ __forceinline__ double bp(double a, double b, const Tab &T) { return box_plus_strict(a, b, T); }
+    using Regs = GlibcK;
+    static __device__ __forceinline__ Regs regs() { return GlibcK::pinned(); }
+    static __device__ __forceinline__ double bp(double a, double b, const Tab &T, const Regs &K) {
+        return box_plus_strict(a, b, T, K);
+    }
 };
 
 // Edge-message access: NT = non-temporal (streamed once per sweep; keeps the
@@ -160,19 +169,19 @@ struct CheckIn {
 // decoder.pyx:341-367, one live B instead of D.  Lane byte offset b8 = f * 8.
 template <int AR, int D, bool NT>
 __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m)[D], int base, uint8_t sb, uint32_t b8,
-                                            const typename Arith<AR>::Tab &tab) {
+                                            const typename Arith<AR>::Tab &tab, const typename Arith<AR>::Regs &K) {
     const int ld = a.ld;
     const double s = sb ? -1.0 : 1.0;
     double F[D - 1];
     F[0] = m[0];
 #pragma unroll
-    for (int i = 1; i < D - 1; ++i) F[i] = Arith<AR>::bp(F[i - 1], m[i], tab);
+    for (int i = 1; i < D - 1; ++i) F[i] = Arith<AR>::bp(F[i - 1], m[i], tab, K);
     st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + D - 1], ld), b8), s * F[D - 2]);
     double Bn = m[D - 1];
 #pragma unroll
     for (int i = D - 2; i > 0; --i) {
-        st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), s * Arith<AR>::bp(F[i - 1], Bn, tab));
-        Bn = Arith<AR>::bp(Bn, m[i], tab);
+        st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), s * Arith<AR>::bp(F[i - 1], Bn, tab, K));
+        Bn = Arith<AR>::bp(Bn, m[i], tab, K);
     }
     st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base], ld), b8), s * Bn);
 }
@@ -202,6 +211,7 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
     int64_t ci = (int64_t)bx * a.g.per * nsub + sub;
     if (ci >= a.n_checks) return;
     uint32_t bad = 0;
+    const auto K = Arith<AR>::regs();
     CheckIn<D, MODE, NT> nx;
     nx.load(a, ci, f);
     for (int j = 0; j < a.g.per; ++j) {
@@ -234,10 +244,10 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
                         st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), v);
                     });
                 } else {
-                    check_exact<kFast, D, NT>(a, m, cur.base, cur.sb, b8, tab);
+                    check_exact<kFast, D, NT>(a, m, cur.base, cur.sb, b8, tab, Arith<kFast>::Regs{});
                 }
             } else {
-                check_exact<AR, D, NT>(a, m, cur.base, cur.sb, b8, tab);
+                check_exact<AR, D, NT>(a, m, cur.base, cur.sb, b8, tab, K);
             }
         }
         if (!more) break;
@@ -338,11 +348,12 @@ __device__ __forceinline__ void check_update_generic(int d, const double *m, dou
                                                      const typename Arith<AR>::Tab &tab) {
     double F[kMaxGenericDeg], Bk[kMaxGenericDeg];
     F[0] = m[0];
-    for (int i = 1; i < d - 1; ++i) F[i] = Arith<AR>::bp(F[i - 1], m[i], tab);
+    const auto K = Arith<AR>::regs();
+    for (int i = 1; i < d - 1; ++i) F[i] = Arith<AR>::bp(F[i - 1], m[i], tab, K);
     Bk[d - 1] = m[d - 1];
-    for (int i = d - 2; i > 0; --i) Bk[i] = Arith<AR>::bp(Bk[i + 1], m[i], tab);
+    for (int i = d - 2; i > 0; --i) Bk[i] = Arith<AR>::bp(Bk[i + 1], m[i], tab, K);
     out[0] = s * Bk[1];
-    for (int i = 1; i < d - 1; ++i) out[i] = s * Arith<AR>::bp(F[i - 1], Bk[i + 1], tab);
+    for (int i = 1; i < d - 1; ++i) out[i] = s * Arith<AR>::bp(F[i - 1], Bk[i + 1], tab, K);
     out[d - 1] = s * F[d - 2];
 }
 

@@ -38,7 +38,9 @@
 
 namespace qr {
 
-// {tail, sbits} per exp interval and {invc, logc} per log interval: 4 KiB, staged in LDS.
+// {tail_i, S_i} per exp interval and {invc, logc} per log interval: 4 KiB, staged in LDS.
+// S_i = asdouble(tab[2i+1] + (i << 45)) is 2^(i/128) as glibc rounds it: glibc's
+// sbits = tab[2i+1] + (ki << 45) is asuint64(S_i) + (k << 52) with k = ki >> 7.
 struct GlibcTables {
     double2 ex[128];
     double2 lg[128];
@@ -47,7 +49,7 @@ struct GlibcTables {
 inline void build_glibc_tables(GlibcTables *t) {
     for (int i = 0; i < 128; ++i) {
         t->ex[i].x = __builtin_bit_cast(double, kGxTab[2 * i]);
-        t->ex[i].y = __builtin_bit_cast(double, kGxTab[2 * i + 1]);
+        t->ex[i].y = __builtin_bit_cast(double, kGxTab[2 * i + 1] + ((uint64_t)i << 45));
         t->lg[i].x = kGlTab[2 * i];
         t->lg[i].y = kGlTab[2 * i + 1];
     }
@@ -77,7 +79,7 @@ __host__ __device__ __forceinline__ double g_exp(double x, const GlibcTables &T)
     double r = __builtin_fma(kd, kGxNegLn2hiN, x);
     r = __builtin_fma(kd, kGxNegLn2loN, r);
     const double2 e = T.ex[ki & 127u];
-    const double scale = g_make(g_hi(e.y) + (ki << 13), g_lo(e.y));  // sbits = T[2i+1] + (ki << 45)
+    const double scale = g_make(g_hi(e.y) + ((uint32_t)((int)ki >> 7) << 20), g_lo(e.y));  // sbits
     const double r2 = r * r;
     const double p23 = __builtin_fma(r, kGxC3, kGxC2);
     const double tr = e.x + r;
@@ -168,7 +170,7 @@ __host__ __device__ __forceinline__ double g_exp_full(double x, const GlibcTable
     double r = __builtin_fma(kd, kGxNegLn2hiN, x);
     r = __builtin_fma(kd, kGxNegLn2loN, r);
     const double2 e = T.ex[ki & 127u];
-    const uint32_t shi = g_hi(e.y) + (ki << 13), slo = g_lo(e.y);
+    const uint32_t shi = g_hi(e.y) + ((uint32_t)((int)ki >> 7) << 20), slo = g_lo(e.y);
     const double r2 = r * r;
     const double p23 = __builtin_fma(r, kGxC3, kGxC2);
     const double tr = e.x + r;
@@ -239,23 +241,40 @@ __constant__ static const GlibcTables kGlibcConst = QR_GLIBC_TABLES_INIT;
 
 // ---- the box-plus domain: h(t) = log(1.0 + exp(-t)), t >= 0, inf or NaN ----------------
 //
+// GlibcK: the addends of the fmas whose two other operands are constants too.  gfx9
+// VOP3 reads at most one SGPR, so each such fma costs a v_mov of its constant into a
+// VGPR at every use; a kernel that keeps these eight in VGPRs (GlibcK::pinned(), once
+// per thread) saves 8 VALU per h.  Host and default construction: plain constants.
+struct GlibcK {
+    double shift = kGxShift, c2 = kGxC2, c4 = kGxC4, a1 = kGlA1, a3 = kGlA3, b1 = kGlB1, b4 = kGlB4, b7 = kGlB7;
+    __host__ __device__ static GlibcK pinned() {
+        GlibcK k;
+#ifdef __HIP_DEVICE_COMPILE__
+        asm volatile("" : "+v"(k.shift), "+v"(k.c2), "+v"(k.c4), "+v"(k.a1));
+        asm volatile("" : "+v"(k.a3), "+v"(k.b1), "+v"(k.b4), "+v"(k.b7));
+#endif
+        return k;
+    }
+};
+//
 // exp(x) for x in [-37.51, 0] or NaN: g_exp without the |x| < 2^-54 case, which the
-// main path already rounds to exactly 1.0 + x there (= 1.0; tests/native pin it).
-__host__ __device__ __forceinline__ double g_exp_neg(double x, const GlibcTables &T) {
-    double kd = __builtin_fma(x, kGxInvLn2N, kGxShift);
+// main path already rounds to exactly 1.0 + x there (= 1.0; tests/native pin it), and
+// with the scale taken by ldexp (exact for these normal results).
+__host__ __device__ __forceinline__ double g_exp_neg(double x, const GlibcTables &T, const GlibcK &K = GlibcK()) {
+    double kd = __builtin_fma(x, kGxInvLn2N, K.shift);
     const uint32_t ki = g_lo(kd);
     kd = kd - kGxShift;
     double r = __builtin_fma(kd, kGxNegLn2hiN, x);
     r = __builtin_fma(kd, kGxNegLn2loN, r);
     const double2 e = T.ex[ki & 127u];
-    const double scale = g_make(g_hi(e.y) + (ki << 13), g_lo(e.y));
     const double r2 = r * r;
-    const double p23 = __builtin_fma(r, kGxC3, kGxC2);
+    const double p23 = __builtin_fma(r, kGxC3, K.c2);
     const double tr = e.x + r;
-    const double p45 = __builtin_fma(r, kGxC5, kGxC4);
+    const double p45 = __builtin_fma(r, kGxC5, K.c4);
     const double a = __builtin_fma(p23, r2, tr);
     const double r4 = r2 * r2;
     const double tmp = __builtin_fma(r4, p45, a);
+    const double scale = __builtin_ldexp(e.y, (int)ki >> 7);  // exact: the result is normal here
     return __builtin_fma(scale, tmp, scale);
 }
 
@@ -263,14 +282,14 @@ __host__ __device__ __forceinline__ double g_exp_neg(double x, const GlibcTables
 // mantissa z = u 2^-k taken by ldexp (exact; it also carries a NaN through, which
 // the bit arithmetic would not), and without the u == 1 early return (both branches
 // return +0 there).
-__host__ __device__ __forceinline__ double g_log_u(double x, const GlibcTables &T) {
+__host__ __device__ __forceinline__ double g_log_u(double x, const GlibcTables &T, const GlibcK &K = GlibcK()) {
     const uint32_t hx = g_hi(x);
     if (hx < 0x3FF10900u) {  // u in [1, 1 + 0x1.09p-4): the near-1 branch
         const double r = x - 1.0;
-        double p2 = __builtin_fma(r, kGlB2, kGlB1);
-        double p5 = __builtin_fma(r, kGlB5, kGlB4);
+        double p2 = __builtin_fma(r, kGlB2, K.b1);
+        double p5 = __builtin_fma(r, kGlB5, K.b4);
         const double r2 = r * r;
-        double p8 = __builtin_fma(r, kGlB8, kGlB7);
+        double p8 = __builtin_fma(r, kGlB8, K.b7);
         p2 = __builtin_fma(r2, kGlB3, p2);
         p5 = __builtin_fma(r2, kGlB6, p5);
         const double r3 = r * r2;
@@ -297,14 +316,14 @@ __host__ __device__ __forceinline__ double g_log_u(double x, const GlibcTables &
     const double r = __builtin_fma(z, c.x, -1.0);
     const double kd = (double)k;
     const double w = __builtin_fma(kd, kGlLn2hi, c.y);
-    const double pA = __builtin_fma(r, kGlA2, kGlA1);
+    const double pA = __builtin_fma(r, kGlA2, K.a1);
     const double hi = r + w;
     const double r2 = r * r;
     double lo = w - hi;
     lo = lo + r;
     lo = __builtin_fma(kd, kGlLn2lo, lo);
     const double r3 = r * r2;
-    double pB = __builtin_fma(r, kGlA4, kGlA3);
+    double pB = __builtin_fma(r, kGlA4, K.a3);
     lo = __builtin_fma(r2, kGlA0, lo);
     pB = __builtin_fma(pB, r2, pA);
     return __builtin_fma(r3, pB, lo) + hi;
@@ -314,9 +333,9 @@ __host__ __device__ __forceinline__ double g_log_u(double x, const GlibcTables &
 // [37.5, 37.5 + 2^-15) by replacing its high word (there exp(-t) < 2^-54, so
 // 1.0 + exp(-t) == 1.0 and log(1.0) == 0, exactly what the reference returns for
 // every t >= 36.74, inf included); NaN fails the compare and propagates.
-__host__ __device__ __forceinline__ double h_strict(double t, const GlibcTables &T) {
+__host__ __device__ __forceinline__ double h_strict(double t, const GlibcTables &T, const GlibcK &K = GlibcK()) {
     const double tc = g_make((t > 37.5) ? 0x4042C000u : g_hi(t), g_lo(t));
-    return g_log_u(1.0 + g_exp_neg(-tc, T), T);
+    return g_log_u(1.0 + g_exp_neg(-tc, T, K), T, K);
 }
 
 // decoder.pyx:41-45: (sgn(a)sgn(b) * min + h(|a+b|)) - h(|a-b|), each operation
@@ -330,17 +349,18 @@ __host__ __device__ __forceinline__ double h_strict(double t, const GlibcTables 
 #ifndef QR_STRICT_MAXMIN
 #define QR_STRICT_MAXMIN 1
 #endif
-__host__ __device__ __forceinline__ double box_plus_strict(double a, double b, const GlibcTables &T) {
+__host__ __device__ __forceinline__ double box_plus_strict(double a, double b, const GlibcTables &T,
+                                                          const GlibcK &K = GlibcK()) {
     const double m = fmin(fabs(a), fabs(b));
     const double ab = a * b;
     const double sm = copysign(m, ab);
 #if QR_STRICT_MAXMIN
-    const double hp = h_strict(fabs(a) + fabs(b), T);
-    const double hm = h_strict(fabs(fabs(a) - fabs(b)), T);
+    const double hp = h_strict(fabs(a) + fabs(b), T, K);
+    const double hm = h_strict(fabs(fabs(a) - fabs(b)), T, K);
     const bool same = !(ab < 0.0);
     return (sm + (same ? hp : hm)) - (same ? hm : hp);
 #else
-    return (sm + h_strict(fabs(a + b), T)) - h_strict(fabs(a - b), T);
+    return (sm + h_strict(fabs(a + b), T, K)) - h_strict(fabs(a - b), T, K);
 #endif
 }
 
