@@ -15,9 +15,16 @@ A "step" = one pass of the hot path over one batch of B frames resident in HBM:
 Inputs (symbols, AWGN, Bob's x_hat/n_hat/word/syndrome, and for dvbs2_4pam the
 LAPPRs) are generated on the GPU before the timed region.
 
-The JSON line carries the roofline of the dominant kernel (the degree-7 check
-sweep k_check<7>, timed with hipEvents on its launch stream inside the timed
-region) and a CPU baseline (the oracle restatement, OpenMP over frames, on a
+Arithmetic (--math): "strict" (default) reproduces the reference's glibc exp/log bit
+for bit, so every output of the measured step equals the reference's; "fast" / "eps"
+are the opt-in approximations (1e-6 on LAPPRs at configs[2], not at configs[3]).  At
+N=1 the line also carries their throughput on the same batch ("alt_math").
+
+The JSON line carries the roofline of the dominant kernel (k_fused<7>: the degree-7
+check sweep of one frame half fused with the variable sweep of the other, timed with
+hipEvents on its launch stream inside the timed region) -- HBM bytes and, because
+the strict check sweep is fp64-VALU bound, its VALU issue rate from the committed
+PMC counts -- and a CPU baseline (the oracle restatement, OpenMP over frames, on a
 bounded sample, rank 0 at N=1 only).
 """
 from __future__ import annotations
@@ -35,6 +42,10 @@ sys.path.insert(0, os.path.join(ROOT, "qam-reconciliation_amd"))
 
 METRIC = "decoded frames/sec @ N=64800, 50 BP iters; achieved HBM GB/s vs roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# fp64 VALU: 78.6 TFLOP/s spec = 1024 SIMDs x 2.4 GHz x 16 fp64 FMA lanes: a wave64 fp64
+# instruction occupies its SIMD 4 cycles, 32-bit VALU 2 cycles (MI355X_MICROARCH.md).
+SIMDS, CLOCK_HZ = 1024, 2.4e9
+MATH = {"strict": 0, "fast": 1, "eps": 2}
 
 
 def parse():
@@ -50,6 +61,8 @@ def parse():
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--no-roofline", action="store_true", help="skip per-kernel event timing")
+    p.add_argument("--math", default="strict", choices=list(MATH), help="decoder arithmetic (strict = bit-exact)")
+    p.add_argument("--no-alt", action="store_true", help="skip the alt_math throughput of the other arithmetics")
     return p.parse_args()
 
 
@@ -203,6 +216,7 @@ def main():
         bps = 4 if args.workload == "dvbs2_16pam" else 2
         snr = args.snr if args.snr is not None else (13.0 if bps == 4 else 3.0)
         code_name = "DVB-S2-rate-1/2-profile IRA N=64800"
+    qamr._lib.tune_set("math", MATH[args.math])
     dec = qamr.Decoder(vid, cid, device=local)
     pipe = SofteningPipeline(dec, bps=bps, snr_db=snr, batch=args.batch, alpha=args.alpha,
                              max_iterations=args.max_iter, device=local)
@@ -282,7 +296,7 @@ def main():
         if kkey:
             avg_s = kstats[kkey]["avg_us"] / 1e6
             ach = bytes_launch / avg_s / 1e9
-            traffic = None
+            traffic, valu = None, None
             pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
             if os.path.exists(pmc):
                 try:
@@ -290,6 +304,15 @@ def main():
                     if t.get("workload") == args.workload and int(t.get("batch", -1)) == batch.B \
                             and t.get("kernel_key") == kkey and t.get("math") == math_mode:
                         traffic = t.get("hbm_bytes_per_launch")
+                        if t.get("valu_insts_per_launch"):
+                            n_all, n64 = t["valu_insts_per_launch"], t.get("valu_f64_insts_per_launch", 0)
+                            busy = (4 * n64 + 2 * (n_all - n64)) / SIMDS / CLOCK_HZ  # s of SIMD issue time
+                            valu = {"wave_insts_per_launch": int(n_all), "f64_wave_insts_per_launch": int(n64),
+                                    "issue_ms_at_2.4GHz": round(busy * 1e3, 3),
+                                    "frac": round(busy / avg_s, 4),
+                                    "note": "SIMD issue time of the launch's VALU instructions (f64 4 cyc, "
+                                            "other 2 cyc per wave64) / launch time; counts from "
+                                            "profiles/pmc_traffic.json (rocprofv3 --pmc)"}
                 except Exception:
                     traffic = None
             copy_gbps = copy_bandwidth(dev) if rank == 0 else None
@@ -298,12 +321,32 @@ def main():
                     "bytes_per_launch": int(bytes_launch), "avg_launch_us": round(avg_s * 1e6, 1),
                     "launches": kstats[kkey]["launches"],
                     "measured_copy_GBps": round(copy_gbps, 1) if copy_gbps else None,
-                    "frac_of_copy": round(ach / copy_gbps, 4) if copy_gbps else None}
+                    "frac_of_copy": round(ach / copy_gbps, 4) if copy_gbps else None, "valu": valu}
     # whole-decode algorithmic bandwidth (SURVEY.md 8(d) B_frame at the iterations actually run)
     it_mean = float(its.float().mean().item())
     V, C, E = dec.vnum, dec.cnum, dec.ednum
     B_it = 24 * E + 24 * V + C
     B_frame = 16 * V + C + it_mean * B_it
+
+    # the other arithmetics on the same resident batch (N=1 only; not the measured value)
+    alt = None
+    if world == 1 and not args.no_alt:
+        alt = {}
+        for name, code in MATH.items():
+            if name == args.math:
+                continue
+            qamr._lib.tune_set("math", code)
+            step()
+            torch.cuda.synchronize(dev)
+            n_alt = 2
+            ta = time.perf_counter()
+            for _ in range(n_alt):
+                step()
+            torch.cuda.synchronize(dev)
+            alt[name] = round(batch.B * n_alt / (time.perf_counter() - ta), 1)
+        qamr._lib.tune_set("math", MATH[args.math])
+        step()  # leave `final` as the measured arithmetic produced it
+        torch.cuda.synchronize(dev)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -320,9 +363,14 @@ def main():
             "data": "synthetic (GPU-generated AWGN softening frames, torch Philox RNG)",
             "config": {"workload": args.workload, "code": code_name, "V": V, "C": C, "E": E,
                        "batch_per_gpu": batch.B, "global_batch": world * batch.B, "max_iterations": args.max_iter,
-                       "snr_db": snr, "bps": bps, "fused_demap": fused, "parallelism": f"dp{world}"},
+                       "snr_db": snr, "bps": bps, "fused_demap": fused, "parallelism": f"dp{world}",
+                       "arithmetic": args.math + (" (glibc exp/log restated: outputs bit-identical to the reference)"
+                                                  if args.math == "strict" else " (approximate, opt-in)")},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "alt_math": {"frames_per_s": alt, "note": "opt-in approximate arithmetics, same batch, 2 steps each; "
+                                                      "not bit-exact (1e-6 LAPPR bar met at configs[2] only)"}
+            if alt else None,
             "decode_alg_GBps": round(B_frame * total_frames / elapsed / 1e9, 1),
             "mean_iterations": it_mean,
             "ber_fer": {"ber": ber, "fer": fer, "avg_iters_success": avg_it, "frames_counted": int(counters[4])},

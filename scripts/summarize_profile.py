@@ -65,6 +65,13 @@ def main():
                "hbm_bytes_per_launch": int((2 * fetch + write) * 1024),
                "correction": "2*FETCH_SIZE + WRITE_SIZE, KiB -> bytes (MI355X_MICROARCH.md HBM section)",
                "avg_launch_us_trace": avg_ns.get(args.kernel, 0) / 1e3}
+        avg = lambda n: sum(kc[n]) / len(kc[n]) if kc.get(n) else None  # noqa: E731
+        if avg("SQ_INSTS_VALU"):
+            out["valu_insts_per_launch"] = avg("SQ_INSTS_VALU")
+            f64 = [avg(n) for n in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                                    "SQ_INSTS_VALU_TRANS_F64") if avg(n) is not None]
+            if f64:
+                out["valu_f64_insts_per_launch"] = sum(f64)
         json.dump(out, open(os.path.join(d, "pmc_traffic.json"), "w"), indent=1)
         lines.append(f"\nDominant kernel `{args.kernel}`: HBM traffic per launch "
                      f"{out['hbm_bytes_per_launch'] / 1e9:.2f} GB (2*FETCH + WRITE)")
