@@ -245,11 +245,14 @@ __constant__ static const GlibcTables kGlibcConst = QR_GLIBC_TABLES_INIT;
 // VOP3 reads at most one SGPR, so each such fma costs a v_mov of its constant into a
 // VGPR at every use; a kernel that keeps these eight in VGPRs (GlibcK::pinned(), once
 // per thread) saves 8 VALU per h.  Host and default construction: plain constants.
+#ifndef QR_PIN_K
+#define QR_PIN_K 1
+#endif
 struct GlibcK {
     double shift = kGxShift, c2 = kGxC2, c4 = kGxC4, a1 = kGlA1, a3 = kGlA3, b1 = kGlB1, b4 = kGlB4, b7 = kGlB7;
     __host__ __device__ static GlibcK pinned() {
         GlibcK k;
-#ifdef __HIP_DEVICE_COMPILE__
+#if defined(__HIP_DEVICE_COMPILE__) && QR_PIN_K
         asm volatile("" : "+v"(k.shift), "+v"(k.c2), "+v"(k.c4), "+v"(k.a1));
         asm volatile("" : "+v"(k.a3), "+v"(k.b1), "+v"(k.b4), "+v"(k.b7));
 #endif
