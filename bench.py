@@ -289,8 +289,21 @@ def main():
             kname = f"k_fused<7,Normal,{ar}> (check sweep of one frame half + variable sweep of the other)"
             kkey = "fused_d7"
         elif "check_d7" in kstats:
-            bytes_launch, _ = check_class_bytes(vid, cid, 7, batch.B)
-            kname, kkey = "k_check<7,Normal> (degree-7 check-node sweep)", "check_d7"
+            ar = {0: "kStrict", 1: "kFast", 2: "kEps"}.get(math_mode, "?")
+            if int(qamr._lib.tune_get("split")) >= 3 and batch.ld % 512 == 0:
+                # two-stream schedule: each launch = the check sweep of one frame half; the
+                # variable sweep of the other half runs concurrently on a second stream
+                half = batch.ld // 2
+                fr_c = min(batch.B, half)
+                bc0, _ = check_class_bytes(vid, cid, 7, fr_c)
+                bc1, _ = check_class_bytes(vid, cid, 7, max(batch.B - fr_c, 0))
+                bytes_launch = (bc0 + bc1) / 2
+                kname = (f"k_check<7,Normal,{ar}> (check sweep of one frame half; the variable sweep of the "
+                         f"other half runs concurrently on a second stream)")
+            else:
+                bytes_launch, _ = check_class_bytes(vid, cid, 7, batch.B)
+                kname = f"k_check<7,Normal,{ar}> (degree-7 check-node sweep)"
+            kkey = "check_d7"
         else:
             kkey = None
         if kkey:

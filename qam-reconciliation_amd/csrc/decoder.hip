@@ -445,7 +445,8 @@ static DecodeWs carve(const qr_code *code, int ld, void *base) {
 
 // Runtime tuning knobs (qr_tune_set); defaults picked by scripts/tune.py on MI355X.
 struct Tuning {
-    std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{2}, math{kStrict}, eps_max{40};
+    std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3}, math{kStrict}, eps_max{40},
+        lds_pad_kb{0};
 };
 static Tuning g_tune;
 
@@ -469,6 +470,7 @@ struct Plan {
     DecodeWs w;
     bool nt;
     hipStream_t s;
+    int lds_pad = 0;  // dynamic LDS reserved by each check workgroup (caps their CU residency)
 
     CheckArgs check_args(const DegreeClass &cls, const double *post_in, uint8_t *unsat, int f0, int f1) const {
         CheckArgs a;
@@ -536,9 +538,9 @@ static int launch_check_class(const Plan &P, const DegreeClass &cls, const doubl
                  P.s);
 #define QR_CASE(DD)                                                                    \
     case DD:                                                                           \
-        if (ar == kStrict) k_check<DD, MODE, NT, kStrict><<<grid, 256, 0, P.s>>>(a);   \
-        else if (ar == kEps) k_check<DD, MODE, NT, kEps><<<grid, 256, 0, P.s>>>(a);    \
-        else k_check<DD, MODE, NT, kFast><<<grid, 256, 0, P.s>>>(a);                   \
+        if (ar == kStrict) k_check<DD, MODE, NT, kStrict><<<grid, 256, P.lds_pad, P.s>>>(a);   \
+        else if (ar == kEps) k_check<DD, MODE, NT, kEps><<<grid, 256, P.lds_pad, P.s>>>(a);    \
+        else k_check<DD, MODE, NT, kFast><<<grid, 256, P.lds_pad, P.s>>>(a);                   \
         break;
     bool handled = true;
     QR_DEG_SWITCH(cls.degree, QR_CASE, handled)
@@ -675,6 +677,65 @@ static int run_split(const Plan &P, int max_it) {
     return QR_OK;
 }
 
+// run_split's per-frame order with the check and variable sweeps of the two halves
+// as separate kernels on two streams (split = 3): the caller's stream s runs the
+// check sweeps and status updates, s2 the variable sweeps, events order them:
+//   s : C_A(1) | [wait vB] C_B(t) S_B(t-1) | [wait vA] C_A(t+1) S_A(t) | ...
+//   s2:        | [wait cA] V_A(t)          | [wait cB] V_B(t)           | ...
+// The variable sweep's 12-VGPR waves fill whatever the 128-VGPR check waves leave of
+// each SIMD and stream their messages under the check sweep's fp64 arithmetic (in
+// the fused launch they take whole check-sized slots instead): 5.15 vs 5.35 ms per
+// half-iteration for the strict arithmetic (MI355X, B=4096).  Knob lds_pad_kb reserves
+// LDS per check workgroup to cap their residency (40/48 KB -> 3 per CU: 5.22-5.26 ms;
+// 64 KB -> 2: 5.65 ms; 0 = default).
+static int run_split2(const Plan &P, int max_it) {
+    const qr_code *code = P.code;
+    std::lock_guard<std::mutex> lk(code->mu);
+    if (!code->s2) {
+        QR_HIP(hipStreamCreateWithFlags(&code->s2, hipStreamNonBlocking));
+        for (auto &e : code->ev) QR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    hipEvent_t fork = code->ev[0], cA = code->ev[1], cB = code->ev[2], vA = code->ev[3], vB = code->ev[4];
+    Plan V = P;
+    V.s = code->s2;
+    Plan C = P;
+    C.lds_pad = std::max(0, g_tune.lds_pad_kb.load()) * 1024;
+    const int ld = P.ld, h = ld / 2;
+    const int A0 = 0, A1 = h, B0 = h, B1 = ld;
+    auto row = [&](int t) { return P.w.unsat + (size_t)t * ld; };
+    int rc;
+    QR_HIP(hipEventRecord(fork, P.s));
+    QR_HIP(hipStreamWaitEvent(V.s, fork, 0));
+    if ((rc = launch_checks<kFirst>(C, P.post, row(0), A0, A1))) return rc;
+    QR_HIP(hipEventRecord(cA, P.s));
+    for (int t = 1; t <= max_it; ++t) {
+        QR_HIP(hipStreamWaitEvent(V.s, cA, 0));
+        if ((rc = launch_var<false>(V, A0, A1))) return rc;
+        QR_HIP(hipEventRecord(vA, V.s));
+        if (t == 1) {
+            if ((rc = launch_checks<kFirst>(C, P.post, row(0), B0, B1))) return rc;
+        } else {
+            QR_HIP(hipStreamWaitEvent(P.s, vB, 0));
+            if ((rc = launch_checks<kNormal>(C, P.post, row(t - 1), B0, B1))) return rc;
+            if ((rc = launch_status(P, B0, B1, t - 1, 0, 0, row(t - 1)))) return rc;
+        }
+        QR_HIP(hipEventRecord(cB, P.s));
+        if (t < max_it) {
+            QR_HIP(hipStreamWaitEvent(P.s, vA, 0));
+            if ((rc = launch_checks<kNormal>(C, P.post, row(t), A0, A1))) return rc;
+            if ((rc = launch_status(P, A0, A1, t, 0, 0, row(t)))) return rc;
+            QR_HIP(hipEventRecord(cA, P.s));
+        }
+        QR_HIP(hipStreamWaitEvent(V.s, cB, 0));
+        if ((rc = launch_var<false>(V, B0, B1))) return rc;
+        QR_HIP(hipEventRecord(vB, V.s));
+    }
+    // join: everything after (final parity check, status) follows both sweeps
+    QR_HIP(hipStreamWaitEvent(P.s, vA, 0));
+    QR_HIP(hipStreamWaitEvent(P.s, vB, 0));
+    return QR_OK;
+}
+
 int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr, const uint8_t *synd, int max_it,
                         double *final_post, uint8_t *success, int32_t *iters, void *ws_ptr, size_t ws_size,
                         hipStream_t s) {
@@ -698,8 +759,9 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     if ((rc = launch_var<true>(P, 0, ld))) return rc;
     int max_deg = 0;
     for (const auto &c : code->classes) max_deg = std::max(max_deg, c.degree);
-    const bool split = g_tune.split.load() >= 2 && ld % 512 == 0 && max_deg <= 16;
-    if ((rc = split ? run_split(P, max_it) : run_flat(P, max_it))) return rc;
+    const int sp = g_tune.split.load();
+    const bool split = sp >= 2 && ld % 512 == 0 && max_deg <= 16;
+    if ((rc = !split ? run_flat(P, max_it) : sp >= 3 ? run_split2(P, max_it) : run_split(P, max_it))) return rc;
     // Check after the last sweep; then every frame still running stops with (0, max).
     const int tf = max_it > 0 ? max_it : 0;
     uint8_t *unsat_last = P.w.unsat + (size_t)tf * ld;
@@ -775,6 +837,9 @@ static int free_code(qr_code *c) {
     (void)hipFree(c->d_var_edge);
     (void)hipFree(c->d_mtab);
     (void)hipFree(c->d_gtab);
+    for (auto &e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->s2) (void)hipStreamDestroy(c->s2);
     delete c;
     return QR_OK;
 }
@@ -887,7 +952,7 @@ int qr_tune_set(const char *name, int64_t value) {
     std::atomic<int> *k = n == "check_ft" ? &g_tune.check_ft : n == "check_per" ? &g_tune.check_per
                         : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
                         : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
-                        : n == "math"     ? &g_tune.math     : n == "eps_max"   ? &g_tune.eps_max
+                        : n == "math"     ? &g_tune.math     : n == "lds_pad_kb" ? &g_tune.lds_pad_kb : n == "eps_max"   ? &g_tune.eps_max
                         : n == "demap_fast" ? &g_demap_fast : nullptr;
     if (!k) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     if (value < 0 || value > 4096) return set_error(QR_EVALUE, "tuning value out of range");
@@ -900,7 +965,7 @@ int qr_tune_get(const char *name, int64_t *value) {
     const std::atomic<int> *k = n == "check_ft" ? &g_tune.check_ft : n == "check_per" ? &g_tune.check_per
                               : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
                               : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
-                              : n == "math"     ? &g_tune.math     : n == "eps_max"   ? &g_tune.eps_max
+                              : n == "math"     ? &g_tune.math     : n == "lds_pad_kb" ? &g_tune.lds_pad_kb : n == "eps_max"   ? &g_tune.eps_max
                               : n == "demap_fast" ? &g_demap_fast : nullptr;
     if (!k || !value) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     *value = k->load();

@@ -94,6 +94,12 @@ struct qr_code {
     qr::MathTables *d_mtab = nullptr;  // box-plus exp/log tables (fastmath.hpp)
     qr::GlibcTables *d_gtab = nullptr; // strict box-plus: glibc exp/log data (glibc_math.hpp)
     mutable qr::Scratch scratch;
+    // two-stream schedule (decoder.hip run_split2): a second stream for the variable
+    // sweeps and the events that order the two; created on first use, guarded by mu
+    // while a decode enqueues (concurrent decodes on one code enqueue one at a time).
+    mutable std::mutex mu;
+    mutable hipStream_t s2 = nullptr;
+    mutable hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
 };
 
 struct qr_demap {
