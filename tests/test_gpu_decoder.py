@@ -246,3 +246,41 @@ def test_math_modes(gpu):
             assert_bit_exact(f_p, res[mode][perm])
     finally:
         _lib.tune_set("math", 0)
+
+
+def test_decode_device_graph_capture(gpu):
+    """The batched decode (every schedule, incl. the default two-stream one whose second
+    stream forks from and joins the caller's stream through events) is capturable in a
+    HIP graph: the replay reproduces the eager decode bit for bit."""
+    import torch
+    from qamr import _lib, codes
+
+    vid, cid = codes.regular_code(1008)
+    dec = _decoder(vid, cid)
+    orc = O.OracleCode(vid, cid)
+    rng = np.random.default_rng(21)
+    B = 512
+    sig = rng.uniform(0.55, 0.9, B)[:, None]
+    word = rng.integers(0, 2, (B, 1008)).astype(np.uint8)
+    synd = np.stack([orc.eval_syndrome(w) for w in word])
+    llr = 2 / sig ** 2 * ((1 - 2.0 * word) + sig * rng.standard_normal((B, 1008)))
+    L = torch.from_numpy(llr.T.copy()).cuda()
+    S = torch.from_numpy(synd.T.copy()).cuda()
+    saved = _lib.tune_get("split")
+    try:
+        for split in (3, 2, 1):
+            _lib.tune_set("split", split)
+            ref = [x.clone() for x in dec.decode_device(L, S, B, 30)]  # eager (also allocates)
+            fin = torch.full_like(L, np.nan)
+            succ = torch.zeros(B, dtype=torch.uint8, device="cuda")
+            its = torch.zeros(B, dtype=torch.int32, device="cuda")
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                dec.decode_device(L, S, B, 30, fin, succ, its)
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(succ, ref[1]) and torch.equal(its, ref[2]), split
+            assert torch.equal(fin.view(torch.int64), ref[0].view(torch.int64)), split
+    finally:
+        _lib.tune_set("split", saved)
