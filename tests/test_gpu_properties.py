@@ -148,7 +148,7 @@ def test_full_size_success_implies_syndrome(gpu):
     assert np.array_equal(ok, s[cols] == 1)
 
 
-@pytest.mark.parametrize("bps,snr", [(2, 3.0), (4, 13.0)])
+@pytest.mark.parametrize("bps,snr", [(2, 3.0), (2, 4.0), (4, 13.0), (4, 14.5)])
 def test_full_size_operating_points_bit_exact(gpu, bps, snr):
     """configs[2] / configs[3] frames (GPU-generated, GPU-demapped) decoded by libqamr
     and by the oracle from the same LAPPRs: identical bits after 50 iterations."""
