@@ -691,9 +691,19 @@ static int run_split(const Plan &P, int max_it) {
 static int run_split2(const Plan &P, int max_it) {
     const qr_code *code = P.code;
     std::lock_guard<std::mutex> lk(code->mu);
-    if (!code->s2) {
-        QR_HIP(hipStreamCreateWithFlags(&code->s2, hipStreamNonBlocking));
-        for (auto &e : code->ev) QR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (!code->s2) {  // first use: all or nothing
+        hipStream_t s2 = nullptr;
+        hipEvent_t ev[5] = {};
+        hipError_t e = hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
+        for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+        if (e != hipSuccess) {
+            for (auto x : ev)
+                if (x) (void)hipEventDestroy(x);
+            if (s2) (void)hipStreamDestroy(s2);
+            return set_error(QR_EDEVICE, "decode: second stream: %s", hipGetErrorString(e));
+        }
+        for (int i = 0; i < 5; ++i) code->ev[i] = ev[i];
+        code->s2 = s2;
     }
     hipEvent_t fork = code->ev[0], cA = code->ev[1], cB = code->ev[2], vA = code->ev[3], vB = code->ev[4];
     Plan V = P;
