@@ -138,6 +138,11 @@ __device__ __forceinline__ void stage_tables(typename Arith<AR>::Tab *lds, const
 #ifndef QR_PREFETCH_C
 #define QR_PREFETCH_C 0
 #endif
+// QR_CHECK_PREFETCH=0: the gathers of check j+1 are issued after the arithmetic of
+// check j instead of before it (fewer live VGPRs, no latency hiding of its own).
+#ifndef QR_CHECK_PREFETCH
+#define QR_CHECK_PREFETCH 1
+#endif
 template <int D, int MODE, bool NT>
 struct CheckIn {
     double p[D], c[D];
@@ -229,7 +234,7 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
         struct { int base; uint8_t sb; } cur = {nx.base, nx.sb};
         const int64_t cn = ci + nsub;
         const bool more = (j + 1 < a.g.per) && cn < a.n_checks;   // wave-uniform
-        if (more) nx.load(a, cn, f);
+        if (QR_CHECK_PREFETCH && more) nx.load(a, cn, f);
         if (MODE != kFirst) bad |= (par == 1u) ? 1u : 0u;  // satisfied iff (parity ^ 1) != 0
         if (MODE != kParityOnly) {
             const uint32_t b8 = (uint32_t)f * 8u;
@@ -251,6 +256,7 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
             }
         }
         if (!more) break;
+        if (!QR_CHECK_PREFETCH) nx.load(a, cn, f);
         ci = cn;
     }
     if (MODE != kFirst && bad && act) a.unsat[f] = 1;  // benign race: every writer stores 1
@@ -284,8 +290,12 @@ __device__ __forceinline__ void var_block(const VarArgs &a, unsigned bx, unsigne
     }
 }
 
+#ifndef QR_CHECK_STRICT_WAVES
+#define QR_CHECK_STRICT_WAVES 1
+#endif
 template <int D, int MODE, bool NT, int AR>
-__global__ void __launch_bounds__(256) k_check(CheckArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AR == kStrict ? QR_CHECK_STRICT_WAVES : 1, 8)))
+k_check(CheckArgs a) {
     __shared__ typename Arith<AR>::Tab tab;
     if (MODE != kParityOnly) stage_tables<AR>(&tab, a);
     check_block<D, MODE, NT, AR>(a, blockIdx.x, blockIdx.y, tab);
