@@ -595,12 +595,20 @@ QR_HD void demap_symbol(const DemapTables& t, const MathTables& mt, const GlibcT
 #endif
         double s = 0;
 #ifndef QR_EXPERIMENT_NO_LLR
-        for (int k = 0; k < j; ++k) s += g_exp_full((2 * y - t.a[k] - aj) * (t.a[k] - aj), gt) * t.p[k];
-#endif
-        s += t.p[j];
-#ifndef QR_EXPERIMENT_NO_LLR
-        for (int k = j + 1; k < M; ++k) s += g_exp_full((2 * y - t.a[k] - aj) * (t.a[k] - aj) / t.two_s2, gt) * t.p[k];  // a division, as :512-515
+        // One loop over all M hypotheses in the reference's summation order (k < j,
+        // then p[j], then k > j): lanes of a wave hold different j, so the two
+        // j-bounded loops of the reference would run max(j) + max(M-1-j) ≈ 2(M-1)
+        // exp slots per wave; here it is M. The per-k argument is selected, not
+        // recomputed, so each lane's sum is bit-identical to the two-loop form.
+#pragma unroll 1
+        for (int k = 0; k < M; ++k) {
+            const double e = (2 * y - t.a[k] - aj) * (t.a[k] - aj);
+            const double arg = k < j ? e : e / t.two_s2;   // a division for k > j, as :512-515
+            const double term = k == j ? t.p[j] : g_exp_full(arg, gt) * t.p[k];
+            s += term;
+        }
 #else
+        s += t.p[j];
         s += y * 1e-300;
 #endif
         const double q = t.dF[i] / s;
