@@ -22,7 +22,9 @@ namespace qr {
 std::atomic<int> g_demap_fast{1};
 
 #ifndef QR_DEMAP_WAVES
-#define QR_DEMAP_WAVES 4   // 4 waves/SIMD: 14.2 vs 15.8 ms (4-PAM), 52.9 vs 56.6 ms (16-PAM) per 4096 frames
+// Single-loop LLR sum: 5 waves/SIMD (96 VGPRs, 52-84 B spilled) 53.4 / 58.5 ms vs 4 waves 55.9 / 62.5 ms
+// (16-PAM at 13 / 25 dB, 4096 frames), 4-PAM 14.5 ms either way; 3 waves 55.6 / 62.0 ms.
+#define QR_DEMAP_WAVES 5
 #endif
 template <bool FAST, int BPS>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QR_DEMAP_WAVES, 8))) k_demap(const DemapTables *__restrict__ tab, const MathTables *__restrict__ gmt,
