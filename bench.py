@@ -1,31 +1,41 @@
 #!/usr/bin/env python3
 """Benchmark: decoded frames/s at N=64800, 50 BP iterations (BASELINE.json metric).
 
-One process per GPU (torch.distributed over RCCL for N > 1).  Frames are
-independent, so every rank decodes its own batch (weak scaling; no collective
-on the data path); the only collective is the final all-reduce of the BER/FER
-counters plus the max-over-ranks of the timed region.
+One process per GPU, torch.distributed over RCCL (qamr.dist).  Frames are
+independent, so every rank decodes its own batch of B frames (weak scaling, no
+collective on the data path); the only collectives are the all-reduce of the five
+BER/FER counters and the max over ranks of the timed region.
+
+Launch:
+  python bench.py --gpus N ...            N > 1 without WORLD_SIZE: this process
+                                          starts N fresh rank processes itself
+                                          (before touching the GPU) and waits.
+  torchrun --nproc-per-node N bench.py --gpus N ...
+                                          WORLD_SIZE must equal --gpus.
+  Rehearsal knobs (several ranks on one GPU, or on CPU): QAMR_BENCH_DEVICE=<d> binds
+  every rank to GPU d, QAMR_BENCH_BACKEND=gloo replaces RCCL, QAMR_BENCH_STUB=1
+  replaces the GPU work by a CPU stub (tests/test_dist.py).
 
 A "step" = one pass of the hot path over one batch of B frames resident in HBM:
-  --workload dvbs2_4pam   (default, configs[2]): batched Decoder._decode of B
-                           frames, max_iterations=50, EsN0 3.0 dB (every frame runs
-                           all 50 iterations: the worst case / headline).
+  --workload dvbs2_4pam   (default, configs[2]; configs[4] = the same at N=8):
+                           batched Decoder._decode of B frames, max_iterations=50,
+                           EsN0 3.0 dB (every frame runs all 50 iterations).
   --workload dvbs2_16pam  (configs[3]): fused NoiseMapper soft demap (16-PAM) ->
                            decode of B frames.
-Inputs (symbols, AWGN, Bob's x_hat/n_hat/word/syndrome, and for dvbs2_4pam the
-LAPPRs) are generated on the GPU before the timed region.
+  --workload reg1008_4pam (configs[1]).
+Inputs (symbols, AWGN, Bob's x_hat/n_hat/word/syndrome, and for the unfused
+workloads the LAPPRs) are generated on the GPU before the timed region.
 
-Arithmetic (--math): "strict" (default) reproduces the reference's glibc exp/log bit
-for bit, so every output of the measured step equals the reference's; "fast" / "eps"
-are the opt-in approximations (1e-6 on LAPPRs at configs[2], not at configs[3]).  At
-N=1 the line also carries their throughput on the same batch ("alt_math").
-
-The JSON line carries the roofline of the dominant kernel (k_fused<7>: the degree-7
-check sweep of one frame half fused with the variable sweep of the other, timed with
-hipEvents on its launch stream inside the timed region) -- HBM bytes and, because
-the strict check sweep is fp64-VALU bound, its VALU issue rate from the committed
-PMC counts -- and a CPU baseline (the oracle restatement, OpenMP over frames, on a
-bounded sample, rank 0 at N=1 only).
+At N=1 the line also carries
+  * roofline  -- the dominant kernel's algorithmic bytes / its hipEvent-timed launch
+                 (on its launch stream, inside the timed region), the PMC traffic and
+                 VALU issue fraction from profiles/pmc_traffic.json; "bound" names
+                 the larger of the HBM and the fp64-VALU fractions;
+  * secondary -- configs[1], configs[3] and the converging operating points
+                 (4-PAM 4.0 dB, 16-PAM 14.5 dB), each timed separately;
+  * cpu_baseline -- the oracle restatement (OpenMP over frames) on a bounded sample,
+                 with its speed ratio to the Cython reference measured in the build
+                 container (profiles/cpu_calibration.json).
 """
 from __future__ import annotations
 
@@ -40,6 +50,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "qam-reconciliation_amd"))
 
+from qamr import dist  # noqa: E402  (pure Python; touches no GPU)
+
 METRIC = "decoded frames/sec @ N=64800, 50 BP iters; achieved HBM GB/s vs roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # fp64 VALU: 78.6 TFLOP/s spec = 1024 SIMDs x 2.4 GHz x 16 fp64 FMA lanes: a wave64 fp64
@@ -47,8 +59,19 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SIMDS, CLOCK_HZ = 1024, 2.4e9
 MATH = {"strict": 0, "fast": 1, "eps": 2}
 
+# (name, workload, snr, batch, steps, BASELINE.json config it measures)
+SECONDARY = [
+    ("configs1_reg1008_4pam", "reg1008_4pam", 3.0, 1024, 5, "configs[1]: reg-(3,6) N=1008, 4-PAM, B=1024"),
+    ("configs3_dvbs2_16pam", "dvbs2_16pam", 13.0, 4096, 3,
+     "configs[3]: N=64800 16-PAM, demap fused into the step, B=4096, 13 dB (all 50 iterations)"),
+    ("op_dvbs2_4pam_4.0dB", "dvbs2_4pam", 4.0, 4096, 3,
+     "configs[2] code at its converging operating point 4.0 dB (frames stop early)"),
+    ("op_dvbs2_16pam_14.5dB", "dvbs2_16pam", 14.5, 4096, 3,
+     "configs[3] at its converging operating point 14.5 dB (demap fused)"),
+]
 
-def parse():
+
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
@@ -63,43 +86,11 @@ def parse():
     p.add_argument("--no-roofline", action="store_true", help="skip per-kernel event timing")
     p.add_argument("--math", default="strict", choices=list(MATH), help="decoder arithmetic (strict = bit-exact)")
     p.add_argument("--no-alt", action="store_true", help="skip the alt_math throughput of the other arithmetics")
-    return p.parse_args()
+    p.add_argument("--no-secondary", action="store_true", help="skip the secondary configs")
+    return p.parse_args(argv)
 
 
-def setup_dist(args):
-    import torch
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # Rehearsal knobs (several ranks on a 1-GPU box): QAMR_BENCH_DEVICE pins every
-    # rank to one device, QAMR_BENCH_BACKEND=gloo replaces RCCL (which refuses two
-    # ranks on one GPU).  The driver's N-GPU runs use neither.
-    local = int(os.environ.get("QAMR_BENCH_DEVICE", local))
-    if world > 1:
-        import torch.distributed as dist
-
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        if os.environ.get("QAMR_BENCH_BACKEND", "nccl") == "gloo":
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return world, rank, local
-
-
-def reduce_(t, op):
-    """All-reduce a small GPU tensor (via the host under gloo)."""
-    import torch.distributed as dist
-
-    if dist.get_backend() == "gloo":
-        h = t.cpu()
-        dist.all_reduce(h, op=op)
-        t.copy_(h)
-    else:
-        dist.all_reduce(t, op=op)
-
-
+# --------------------------------------------------------------------- bytes
 def var_sweep_bytes(V, E, B):
     """Algorithmic bytes of one variable sweep over B frames: c2v read (8 B per
     edge), lappr read and post write (8 B per variable each) -- SURVEY.md 8(d)."""
@@ -120,47 +111,114 @@ def check_class_bytes(vid, cid, degree, B):
     return (16 * E_d + 8 * V_d + C_d) * B + B, dict(E=E_d, V=V_d, C=C_d)
 
 
-def cpu_baseline(args, vid, cid, pipe, batch, lappr_host_fn, budget_s):
-    """Oracle restatement on the host cores for ~budget_s seconds of the same workload."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
+# ----------------------------------------------------------------- rank body
+def timed_region(step, sync, steps, warmup, before=None, after=None):
+    """W untimed warmup steps, then EXACTLY K steps bracketed by a barrier + device
+    sync on both sides; returns the max over ranks of the timed region [s]."""
+    import torch
 
-    try:
-        aff = len(os.sched_getaffinity(0))
-    except Exception:
-        aff = os.cpu_count() or 1
-    cores = max(1, min(aff, int(os.environ.get("OMP_NUM_THREADS", aff))))
-    code = O.OracleCode(vid, cid)
-    nfr = min(batch.B, cores)
-    synd = batch.synd[:, :nfr].cpu().numpy().T.copy()
-    if args.workload == "dvbs2_16pam":
-        nm = O.OracleNoiseMapper(4, 2.0, pipe.noise_var, np.array([0, 1] * 8, np.uint8))
-        nh = batch.nhat[:, :nfr].cpu().numpy().T.copy()
-        xs = batch.x[:, :nfr].cpu().numpy().T.copy()
-    else:
-        L = lappr_host_fn(nfr)
-    frames, t0 = 0, time.perf_counter()
-    rounds = 0
-    while True:
-        if args.workload == "dvbs2_16pam":
-            L = np.stack([nm.demap_lappr_array(nh[f], xs[f], nthreads=cores) * args.alpha for f in range(nfr)])
-        code.decode_batch(L, synd, args.max_iter, nthreads=cores)
-        frames += nfr
-        rounds += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or rounds >= 50:
-            break
-    cpu_model = ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu_model = line.split(":", 1)[1].strip()
-                break
-    except Exception:
+    for _ in range(warmup):
+        step()
+    sync()
+    if before:
+        before()
+    dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if after:
+        after()
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce_max(t)
+    return float(t.item())
+
+
+class StubWork:
+    """CPU stand-in for the GPU step (QAMR_BENCH_STUB=1): exercises the launcher,
+    the timed region and the counter reduction of the real rank body."""
+
+    def __init__(self, args, rank):
+        self.args, self.rank = args, rank
+        self.B = args.batch
+        self.V, self.C, self.E = 1008, 504, 3024
+
+    def step(self):
+        time.sleep(0.002)
+
+    def sync(self):
         pass
-    return {"value": frames / el, "unit": "frames/s", "cores": cores, "kind": "port",
-            "sample": f"{frames} frames ({rounds} rounds x {nfr}) of the same workload in {el:.1f} s, "
-                      f"oracle/qamr_oracle.c (gcc -O2 -ffp-contract=off, OpenMP over frames) on {cpu_model}"}
+
+    def counters(self):
+        import torch
+
+        r = self.rank
+        return torch.tensor([10 * (r + 1), r + 1, self.B - r - 1, 7 * (self.B - r - 1), self.B], dtype=torch.int64)
+
+
+class Work:
+    """One workload on one GPU: code, softening pipeline, a batch resident in HBM."""
+
+    def __init__(self, workload, snr, batch, max_iter, alpha, seed, rank, local):
+        import torch
+
+        import qamr
+        from qamr import codes
+        from qamr.pipeline import SofteningPipeline
+
+        self.workload = workload
+        if workload == "reg1008_4pam":
+            self.vid, self.cid = codes.regular_code(1008)
+            bps, snr = 2, (3.0 if snr is None else snr)
+            self.code_name = "reg-(3,6) N=1008"
+        else:
+            self.vid, self.cid = codes.dvbs2_like_half()
+            bps = 4 if workload == "dvbs2_16pam" else 2
+            snr = snr if snr is not None else (13.0 if bps == 4 else 3.0)
+            self.code_name = "DVB-S2-rate-1/2-profile IRA N=64800"
+        self.bps, self.snr, self.max_iter, self.alpha = bps, snr, max_iter, alpha
+        self.dev = torch.device("cuda", local)
+        self.dec = qamr.Decoder(self.vid, self.cid, device=local)
+        self.pipe = SofteningPipeline(self.dec, bps=bps, snr_db=snr, batch=batch, alpha=alpha,
+                                      max_iterations=max_iter, device=local)
+        gen = torch.Generator(device=self.dev).manual_seed(seed * 1000 + rank)
+        self.batch = self.pipe.generate(gen)
+        self.B = self.batch.B
+        self.fused = workload == "dvbs2_16pam"
+        self.lappr = self.pipe.demap(self.batch)  # input LAPPRs (re-computed inside each step when fused)
+        self.final = torch.empty_like(self.lappr)
+        self.succ = torch.empty(self.B, dtype=torch.uint8, device=self.dev)
+        self.its = torch.empty(self.B, dtype=torch.int32, device=self.dev)
+        self.V, self.C, self.E = self.dec.vnum, self.dec.cnum, self.dec.ednum
+        torch.cuda.synchronize(self.dev)
+
+    def step(self):
+        if self.fused:
+            self.pipe.demap(self.batch, out=self.lappr)
+        self.pipe.decode(self.lappr, self.batch, self.final, self.succ, self.its)
+
+    def sync(self):
+        import torch
+
+        torch.cuda.synchronize(self.dev)
+
+    def counters(self):
+        self.pipe.counters.zero_()
+        self.pipe.count(self.final, self.batch, self.succ, self.its)
+        return self.pipe.counters.clone()
+
+    def mean_iterations(self):
+        return float(self.its.float().mean().item())
+
+    def free(self):
+        import torch
+
+        for k in ("batch", "lappr", "final", "succ", "its", "pipe", "dec"):
+            setattr(self, k, None)
+        torch.cuda.empty_cache()
 
 
 def copy_bandwidth(dev, nbytes=2 << 30, reps=5):
@@ -168,6 +226,7 @@ def copy_bandwidth(dev, nbytes=2 << 30, reps=5):
     libqamr's 16-B-per-lane copy kernel): the practical HBM ceiling SURVEY.md 8(d)
     asks the roofline to be related to."""
     import ctypes
+
     import torch
     from qamr import _lib
 
@@ -193,192 +252,268 @@ def copy_bandwidth(dev, nbytes=2 << 30, reps=5):
     return gbps
 
 
-def main():
-    args = parse()
+def kernel_stats():
+    import qamr
+
+    out = {}
+    for k in ("check", "check_d7", "check_d6", "check1", "fused_d7", "var", "var_init", "parity", "status", "demap",
+              "repack"):
+        ms, n = qamr.profile_query(k)
+        if n:
+            out[k] = {"avg_us": 1e3 * ms / n, "launches": n, "total_ms": ms}
+    return out
+
+
+def roofline(args, w, kstats, dev):
+    """The dominant kernel's algorithmic bytes per launch / its average launch time."""
+    import qamr
+
+    math_mode = int(qamr._lib.tune_get("math"))
+    ar = {0: "kStrict", 1: "kFast", 2: "kEps"}.get(math_mode, "?")
+    B, ld = w.B, w.batch.ld
+    if "fused_d7" in kstats:
+        # split = 2: one launch = check sweep of one frame half + variable sweep of the other
+        half = ld // 2
+        fr_c = min(B, half)
+        fr_v = B - fr_c if B > half else 0
+        bc0, _ = check_class_bytes(w.vid, w.cid, 7, fr_c)
+        bc1, _ = check_class_bytes(w.vid, w.cid, 7, max(B - fr_c, 0))
+        bytes_launch = (bc0 + bc1) / 2 + (var_sweep_bytes(w.V, w.E, fr_c) + var_sweep_bytes(w.V, w.E, fr_v)) / 2
+        kname = f"k_fused<7,Normal,{ar}> (check sweep of one frame half + variable sweep of the other)"
+        kkey = "fused_d7"
+    elif "check_d7" in kstats:
+        if int(qamr._lib.tune_get("split")) >= 3 and ld % 512 == 0:
+            # two-stream schedule: each launch = the check sweep of one frame half; the
+            # variable sweep of the other half runs concurrently on a second stream
+            half = ld // 2
+            fr_c = min(B, half)
+            bc0, _ = check_class_bytes(w.vid, w.cid, 7, fr_c)
+            bc1, _ = check_class_bytes(w.vid, w.cid, 7, max(B - fr_c, 0))
+            bytes_launch = (bc0 + bc1) / 2
+            kname = (f"k_check<7,Normal,{ar}> (check sweep of one frame half; the variable sweep of the "
+                     f"other half runs concurrently on a second stream)")
+        else:
+            bytes_launch, _ = check_class_bytes(w.vid, w.cid, 7, B)
+            kname = f"k_check<7,Normal,{ar}> (degree-7 check-node sweep)"
+        kkey = "check_d7"
+    else:
+        return None
+    avg_s = kstats[kkey]["avg_us"] / 1e6
+    ach = bytes_launch / avg_s / 1e9
+    traffic, valu = None, None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            t = json.load(open(pmc))
+            if t.get("workload") == args.workload and int(t.get("batch", -1)) == B \
+                    and t.get("kernel_key") == kkey and t.get("math") == math_mode:
+                traffic = t.get("hbm_bytes_per_launch")
+                if t.get("valu_insts_per_launch"):
+                    n_all, n64 = t["valu_insts_per_launch"], t.get("valu_f64_insts_per_launch", 0)
+                    busy = (4 * n64 + 2 * (n_all - n64)) / SIMDS / CLOCK_HZ  # s of SIMD issue time
+                    valu = {"wave_insts_per_launch": int(n_all), "f64_wave_insts_per_launch": int(n64),
+                            "issue_ms_at_2.4GHz": round(busy * 1e3, 3),
+                            "frac": round(busy / avg_s, 4),
+                            "source": t.get("source"),
+                            "note": "SIMD issue time of the launch's VALU instructions (f64 4 cyc, "
+                                    "other 2 cyc per wave64) / measured launch time; counts from "
+                                    "profiles/pmc_traffic.json (rocprofv3 --pmc)"}
+        except Exception:
+            traffic = None
+    copy_gbps = copy_bandwidth(dev)
+    frac = ach / HBM_PEAK_GBS
+    bound = "valu" if valu and valu["frac"] > frac else "hbm"
+    return {"bound": bound, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(frac, 4), "traffic": traffic, "kernel": kname,
+            "bytes_per_launch": int(bytes_launch), "avg_launch_us": round(avg_s * 1e6, 1),
+            "launches": kstats[kkey]["launches"],
+            "measured_copy_GBps": round(copy_gbps, 1), "frac_of_copy": round(ach / copy_gbps, 4), "valu": valu}
+
+
+def secondary(args, rank, local):
+    """configs[1], configs[3] and the converging operating points, each on its own
+    resident batch, timed separately from the headline (same step definition)."""
     import torch
 
-    world, rank, local = setup_dist(args)
-    import qamr
-    from qamr import codes
-    from qamr.pipeline import SofteningPipeline
+    out = {}
+    for name, wl, snr, batch, steps, what in SECONDARY:
+        w = Work(wl, snr, batch, args.max_iter, args.alpha, args.seed, rank, local)
+        el = timed_region(w.step, w.sync, steps, 1)
+        out[name] = {"frames_per_s": round(w.B * steps / el, 1), "ms_per_step": round(1e3 * el / steps, 3),
+                     "steps": steps, "batch": w.B, "snr_db": w.snr, "mean_iterations": round(w.mean_iterations(), 3),
+                     "what": what}
+        w.free()
+        del w
+        torch.cuda.empty_cache()
+    return out
 
-    if qamr.device_count() <= 0:
-        raise SystemExit("bench: no HIP device")
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
 
-    if args.workload == "reg1008_4pam":
-        vid, cid = codes.regular_code(1008)
-        bps, snr = 2, (3.0 if args.snr is None else args.snr)
-        code_name = "reg-(3,6) N=1008"
+def cpu_calibration():
+    p = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+    try:
+        return json.load(open(p))
+    except Exception:
+        return None
+
+
+def cpu_baseline(args, w, budget_s):
+    """Oracle restatement on the host cores for ~budget_s seconds of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = os.cpu_count() or 1
+    cores = max(1, min(aff, int(os.environ.get("OMP_NUM_THREADS", aff))))
+    code = O.OracleCode(w.vid, w.cid)
+    nfr = min(w.B, cores)
+    synd = w.batch.synd[:, :nfr].cpu().numpy().T.copy()
+    if w.fused:
+        nm = O.OracleNoiseMapper(w.bps, 2.0, w.pipe.noise_var, np.array([0, 1] * (1 << w.bps >> 1), np.uint8))
+        nh = w.batch.nhat[:, :nfr].cpu().numpy().T.copy()
+        xs = w.batch.x[:, :nfr].cpu().numpy().T.copy()
     else:
-        vid, cid = codes.dvbs2_like_half()
-        bps = 4 if args.workload == "dvbs2_16pam" else 2
-        snr = args.snr if args.snr is not None else (13.0 if bps == 4 else 3.0)
-        code_name = "DVB-S2-rate-1/2-profile IRA N=64800"
+        L = w.lappr[:, :nfr].cpu().numpy().T.copy()
+    frames, t0, rounds = 0, time.perf_counter(), 0
+    while True:
+        if w.fused:
+            L = np.stack([nm.demap_lappr_array(nh[f], xs[f], nthreads=cores) * w.alpha for f in range(nfr)])
+        code.decode_batch(L, synd, args.max_iter, nthreads=cores)
+        frames += nfr
+        rounds += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or rounds >= 50:
+            break
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    value = frames / el
+    out = {"value": value, "unit": "frames/s", "cores": cores, "kind": "port",
+           "sample": f"{frames} frames ({rounds} rounds x {nfr}) of the same workload in {el:.1f} s, "
+                     f"oracle/qamr_oracle.c (gcc -O2 -ffp-contract=off, OpenMP over frames) on {cpu_model}"}
+    cal = cpu_calibration()
+    if cal and args.workload in cal.get("workloads", {}):
+        c = cal["workloads"][args.workload]
+        out["ratio_vs_cython"] = c["ratio_port_over_cython"]
+        out["cython_equivalent_frames_per_s"] = value / c["ratio_port_over_cython"]
+        out["calibration"] = (f"port/Cython speed ratio {c['ratio_port_over_cython']:.3f} measured on 1 core of the "
+                              f"build container ({cal.get('cpu', '?')}) on the same frames: "
+                              "profiles/cpu_calibration.json (scripts/cpu_calibrate.py)")
+    return out
+
+
+def alt_math(args, w):
+    """The other arithmetics on the same resident batch (not the measured value)."""
+    import qamr
+
+    alt = {}
+    for name, code in MATH.items():
+        if name == args.math:
+            continue
+        qamr._lib.tune_set("math", code)
+        w.step()
+        w.sync()
+        n_alt = 2
+        ta = time.perf_counter()
+        for _ in range(n_alt):
+            w.step()
+        w.sync()
+        alt[name] = round(w.B * n_alt / (time.perf_counter() - ta), 1)
     qamr._lib.tune_set("math", MATH[args.math])
-    dec = qamr.Decoder(vid, cid, device=local)
-    pipe = SofteningPipeline(dec, bps=bps, snr_db=snr, batch=args.batch, alpha=args.alpha,
-                             max_iterations=args.max_iter, device=local)
-    gen = torch.Generator(device=dev).manual_seed(args.seed * 1000 + rank)
-    batch = pipe.generate(gen)
-    fused = args.workload == "dvbs2_16pam"
-    lappr = pipe.demap(batch)  # input LAPPRs (re-computed inside each step when fused)
-    final = torch.empty_like(lappr)
-    succ = torch.empty(batch.B, dtype=torch.uint8, device=dev)
-    its = torch.empty(batch.B, dtype=torch.int32, device=dev)
-    torch.cuda.synchronize(dev)
+    w.step()  # leave `final` as the measured arithmetic produced it
+    w.sync()
+    return alt
 
-    def step():
-        if fused:
-            pipe.demap(batch, out=lappr)
-        pipe.decode(lappr, batch, final, succ, its)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    if args.gpus < 1:
+        raise SystemExit("bench: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # Start N fresh rank processes (this process has not touched the GPU) and wait.
+        return dist.launch_local(args.gpus, [os.path.abspath(__file__)] + argv)
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if env_world != args.gpus:
+        raise SystemExit(f"bench: WORLD_SIZE={env_world} but --gpus {args.gpus}; they must agree")
 
-    if not args.no_roofline:
-        qamr.profile_reset()
-        qamr.profile_enable(True)
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
-    qamr.profile_enable(False)
+    stub = os.environ.get("QAMR_BENCH_STUB") == "1"
+    backend = os.environ.get("QAMR_BENCH_BACKEND") or ("gloo" if stub else None)
+    dev_pin = os.environ.get("QAMR_BENCH_DEVICE")
+    world, rank, local = dist.init(backend, None if dev_pin is None else int(dev_pin))
+    local = int(dev_pin) if dev_pin is not None else local
 
-    # BER/FER bookkeeping of the last step (and the only data-path-free collective)
-    pipe.count(final, batch, succ, its)
-    counters = pipe.counters.clone()
-    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        import torch.distributed as dist
+    import torch
 
-        reduce_(t_max, dist.ReduceOp.MAX)
-        reduce_(counters, dist.ReduceOp.SUM)
-    elapsed = float(t_max.item())
-    total_frames = world * batch.B * args.steps
+    if stub:
+        w = StubWork(args, rank)
+    else:
+        import qamr
+
+        if qamr.device_count() <= 0:
+            raise SystemExit("bench: no HIP device")
+        torch.cuda.set_device(local)
+        qamr._lib.tune_set("math", MATH[args.math])
+        w = Work(args.workload, args.snr, args.batch, args.max_iter, args.alpha, args.seed, rank, local)
+
+    prof = not stub and not args.no_roofline
+
+    def before():
+        if prof:
+            import qamr
+            qamr.profile_reset()
+            qamr.profile_enable(True)
+
+    def after():
+        if prof:
+            import qamr
+            qamr.profile_enable(False)
+
+    elapsed = timed_region(w.step, w.sync, args.steps, args.warmup, before, after)
+    counters = w.counters()
+    dist.all_reduce_sum(counters)
+    total_frames = world * w.B * args.steps
     value = total_frames / elapsed
 
-    roof = None
-    kstats = {}
-    if not args.no_roofline:
-        for k in ("check", "check_d7", "check_d6", "check1", "fused_d7", "var", "var_init", "parity", "status",
-                  "demap"):
-            ms, n = qamr.profile_query(k)
-            if n:
-                kstats[k] = {"avg_us": 1e3 * ms / n, "launches": n, "total_ms": ms}
-        V_, E_ = dec.vnum, dec.ednum
-        math_mode = int(qamr._lib.tune_get("math"))
-        if "fused_d7" in kstats:
-            # split schedule: one launch = check sweep of one frame half + variable sweep of the other
-            half = batch.ld // 2
-            fr_c = min(batch.B, half)           # real frames in the checked half (first half)
-            fr_v = batch.B - fr_c if batch.B > half else 0
-            # both orientations alternate; price the average launch over both halves
-            bc0, _ = check_class_bytes(vid, cid, 7, fr_c)
-            bc1, _ = check_class_bytes(vid, cid, 7, max(batch.B - fr_c, 0))
-            bytes_launch = (bc0 + bc1) / 2 + (var_sweep_bytes(V_, E_, fr_c) + var_sweep_bytes(V_, E_, fr_v)) / 2
-            ar = {0: "kStrict", 1: "kFast", 2: "kEps"}.get(math_mode, "?")
-            kname = f"k_fused<7,Normal,{ar}> (check sweep of one frame half + variable sweep of the other)"
-            kkey = "fused_d7"
-        elif "check_d7" in kstats:
-            ar = {0: "kStrict", 1: "kFast", 2: "kEps"}.get(math_mode, "?")
-            if int(qamr._lib.tune_get("split")) >= 3 and batch.ld % 512 == 0:
-                # two-stream schedule: each launch = the check sweep of one frame half; the
-                # variable sweep of the other half runs concurrently on a second stream
-                half = batch.ld // 2
-                fr_c = min(batch.B, half)
-                bc0, _ = check_class_bytes(vid, cid, 7, fr_c)
-                bc1, _ = check_class_bytes(vid, cid, 7, max(batch.B - fr_c, 0))
-                bytes_launch = (bc0 + bc1) / 2
-                kname = (f"k_check<7,Normal,{ar}> (check sweep of one frame half; the variable sweep of the "
-                         f"other half runs concurrently on a second stream)")
-            else:
-                bytes_launch, _ = check_class_bytes(vid, cid, 7, batch.B)
-                kname = f"k_check<7,Normal,{ar}> (degree-7 check-node sweep)"
-            kkey = "check_d7"
-        else:
-            kkey = None
-        if kkey:
-            avg_s = kstats[kkey]["avg_us"] / 1e6
-            ach = bytes_launch / avg_s / 1e9
-            traffic, valu = None, None
-            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-            if os.path.exists(pmc):
-                try:
-                    t = json.load(open(pmc))
-                    if t.get("workload") == args.workload and int(t.get("batch", -1)) == batch.B \
-                            and t.get("kernel_key") == kkey and t.get("math") == math_mode:
-                        traffic = t.get("hbm_bytes_per_launch")
-                        if t.get("valu_insts_per_launch"):
-                            n_all, n64 = t["valu_insts_per_launch"], t.get("valu_f64_insts_per_launch", 0)
-                            busy = (4 * n64 + 2 * (n_all - n64)) / SIMDS / CLOCK_HZ  # s of SIMD issue time
-                            valu = {"wave_insts_per_launch": int(n_all), "f64_wave_insts_per_launch": int(n64),
-                                    "issue_ms_at_2.4GHz": round(busy * 1e3, 3),
-                                    "frac": round(busy / avg_s, 4),
-                                    "note": "SIMD issue time of the launch's VALU instructions (f64 4 cyc, "
-                                            "other 2 cyc per wave64) / launch time; counts from "
-                                            "profiles/pmc_traffic.json (rocprofv3 --pmc)"}
-                except Exception:
-                    traffic = None
-            copy_gbps = copy_bandwidth(dev) if rank == 0 else None
-            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
-                    "bytes_per_launch": int(bytes_launch), "avg_launch_us": round(avg_s * 1e6, 1),
-                    "launches": kstats[kkey]["launches"],
-                    "measured_copy_GBps": round(copy_gbps, 1) if copy_gbps else None,
-                    "frac_of_copy": round(ach / copy_gbps, 4) if copy_gbps else None, "valu": valu}
-    # whole-decode algorithmic bandwidth (SURVEY.md 8(d) B_frame at the iterations actually run)
-    it_mean = float(its.float().mean().item())
-    V, C, E = dec.vnum, dec.cnum, dec.ednum
-    B_it = 24 * E + 24 * V + C
-    B_frame = 16 * V + C + it_mean * B_it
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (GPU-generated AWGN softening frames, torch Philox RNG)" if not stub else "stub",
+    }
+    if stub:
+        out["config"] = {"workload": "stub", "batch_per_gpu": w.B, "global_batch": world * w.B,
+                         "parallelism": f"dp{world}", "backend": dist.backend()}
+        out["counters"] = [int(v) for v in counters]
+    else:
+        from qamr.pipeline import SofteningPipeline
 
-    # the other arithmetics on the same resident batch (N=1 only; not the measured value)
-    alt = None
-    if world == 1 and not args.no_alt:
-        alt = {}
-        for name, code in MATH.items():
-            if name == args.math:
-                continue
-            qamr._lib.tune_set("math", code)
-            step()
-            torch.cuda.synchronize(dev)
-            n_alt = 2
-            ta = time.perf_counter()
-            for _ in range(n_alt):
-                step()
-            torch.cuda.synchronize(dev)
-            alt[name] = round(batch.B * n_alt / (time.perf_counter() - ta), 1)
-        qamr._lib.tune_set("math", MATH[args.math])
-        step()  # leave `final` as the measured arithmetic produced it
-        torch.cuda.synchronize(dev)
-
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        def lappr_host(n):
-            return lappr[:, :n].cpu().numpy().T.copy()
-        cpu = cpu_baseline(args, vid, cid, pipe, batch, lappr_host, args.cpu_seconds)
-
-    if rank == 0:
-        snr_, ber, fer, avg_it = SofteningPipeline.summarize(counters.cpu().numpy(), pipe.K, snr)
-        out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (GPU-generated AWGN softening frames, torch Philox RNG)",
-            "config": {"workload": args.workload, "code": code_name, "V": V, "C": C, "E": E,
-                       "batch_per_gpu": batch.B, "global_batch": world * batch.B, "max_iterations": args.max_iter,
-                       "snr_db": snr, "bps": bps, "fused_demap": fused, "parallelism": f"dp{world}",
-                       "arithmetic": args.math + (" (glibc exp/log restated: outputs bit-identical to the reference)"
-                                                  if args.math == "strict" else " (approximate, opt-in)")},
+        kstats = kernel_stats() if prof else {}
+        roof = roofline(args, w, kstats, w.dev) if (prof and rank == 0) else None
+        it_mean = w.mean_iterations()
+        # whole-decode algorithmic bandwidth (SURVEY.md 8(d) B_frame at the iterations actually run)
+        B_frame = 16 * w.V + w.C + it_mean * (24 * w.E + 24 * w.V + w.C)
+        alt = alt_math(args, w) if (world == 1 and not args.no_alt) else None
+        cpu = None
+        if rank == 0 and world == 1 and args.cpu_seconds > 0:
+            cpu = cpu_baseline(args, w, args.cpu_seconds)
+        snr_, ber, fer, avg_it = SofteningPipeline.summarize(counters.cpu().numpy(), w.pipe.K, w.snr)
+        out["config"] = {"workload": args.workload, "code": w.code_name, "V": w.V, "C": w.C, "E": w.E,
+                         "batch_per_gpu": w.B, "global_batch": world * w.B, "max_iterations": args.max_iter,
+                         "snr_db": w.snr, "bps": w.bps, "fused_demap": w.fused, "parallelism": f"dp{world}",
+                         "backend": dist.backend() or "none",
+                         "arithmetic": args.math + (" (glibc exp/log restated: outputs bit-identical to the "
+                                                    "reference)" if args.math == "strict" else
+                                                    " (approximate, opt-in)")}
+        if dev_pin is not None:
+            out["config"]["rehearsal"] = f"all {world} ranks on GPU {dev_pin}"
+        out.update({
             "roofline": roof,
             "cpu_baseline": cpu,
             "alt_math": {"frames_per_s": alt, "note": "opt-in approximate arithmetics, same batch, 2 steps each; "
@@ -388,11 +523,15 @@ def main():
             "mean_iterations": it_mean,
             "ber_fer": {"ber": ber, "fer": fer, "avg_iters_success": avg_it, "frames_counted": int(counters[4])},
             "kernels": kstats,
-        }
-        print(json.dumps(out))
-    if world > 1:
-        torch.distributed.destroy_process_group()
+        })
+        if world == 1 and not args.no_secondary:
+            w.free()
+            out["secondary"] = secondary(args, rank, local)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.finalize()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

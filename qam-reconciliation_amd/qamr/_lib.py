@@ -162,3 +162,24 @@ def profile_query(name: str):
     ms, n = f64(0), i64(0)
     check(load().qr_profile_query(name.encode(), C.byref(ms), C.byref(n)))
     return float(ms.value), int(n.value)
+
+
+def check_tensor(t, name: str, shape=None, dtype=None, device: int | None = None):
+    """Validate a device tensor before its pointer crosses the C-ABI: the kernels
+    index it as a dense row-major array of `shape` on GPU `device`, so a wrong
+    dtype / shape / stride / device would be read or written out of bounds."""
+    import torch
+
+    if not isinstance(t, torch.Tensor):
+        raise ValueError(f"{name}: expected a torch tensor, got {type(t).__name__}")
+    if dtype is not None and t.dtype != dtype:
+        raise ValueError(f"{name}: dtype {t.dtype}, expected {dtype}")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: shape {tuple(t.shape)}, expected {tuple(shape)}")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: must be a GPU tensor")
+    if device is not None and t.device.index != device:
+        raise ValueError(f"{name}: on cuda:{t.device.index}, expected cuda:{device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous (the kernels assume dense rows)")
+    return t

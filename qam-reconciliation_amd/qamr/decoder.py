@@ -60,7 +60,7 @@ class Decoder:
         check(L.qr_code_info(h, C.byref(v), C.byref(c), C.byref(e), C.byref(dc), C.byref(dv)))
         self._V, self._C, self._E = int(v.value), int(c.value), int(e.value)
         self.max_check_degree, self.max_var_degree = int(dc.value), int(dv.value)
-        self._ws = None  # device workspace (torch tensor) for decode_device
+        self._ws = {}  # per-stream device workspaces of decode_device
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -199,33 +199,58 @@ class Decoder:
                       iters=None, stream=None):
         """Decode B frames resident in HBM (torch tensors, frame-innermost).
 
-        lappr_fi: float64 [V, ld]; synd_fi: uint8 [C, ld]; ld % 64 == 0, B <= ld.
+        lappr_fi: float64 [V, ld]; synd_fi: uint8 [C, ld]; ld % 64 == 0, 0 < B <= ld.
         Returns (final_fi float64 [V, ld], success uint8 [B], iters int32 [B]).
-        Asynchronous on ``stream`` (default: torch's current stream)."""
+        Every tensor must be contiguous and on this decoder's GPU (checked).
+        Asynchronous on ``stream`` (default: torch's current stream).  The message
+        workspace is kept per stream, so calls on different streams never share it."""
         import torch
 
+        from ._lib import check_tensor
+
+        dev = self._device
+        if not isinstance(lappr_fi, torch.Tensor) or lappr_fi.dim() != 2:
+            raise ValueError("decode_device: lappr_fi must be a 2-D tensor [V, ld]")
         V, ld = lappr_fi.shape
-        if V != self._V or synd_fi.shape != (self._C, ld):
+        if V != self._V:
             raise ValueError("decode_device: tensor shapes do not match the code")
-        if lappr_fi.dtype != torch.float64 or synd_fi.dtype != torch.uint8:
-            raise ValueError("decode_device: expected float64 LAPPRs and uint8 syndromes")
-        if not (lappr_fi.is_contiguous() and synd_fi.is_contiguous()):
-            raise ValueError("decode_device: tensors must be contiguous")
-        dev = lappr_fi.device
+        if ld % 64 or not 0 < int(B) <= ld:
+            raise ValueError(f"decode_device: need ld % 64 == 0 and 0 < B <= ld (B={B}, ld={ld})")
+        check_tensor(lappr_fi, "lappr_fi", (self._V, ld), torch.float64, dev)
+        check_tensor(synd_fi, "synd_fi", (self._C, ld), torch.uint8, dev)
+        tdev = lappr_fi.device
         if final_fi is None:
             final_fi = torch.empty_like(lappr_fi)
         if success is None:
-            success = torch.empty(B, dtype=torch.uint8, device=dev)
+            success = torch.empty(B, dtype=torch.uint8, device=tdev)
         if iters is None:
-            iters = torch.empty(B, dtype=torch.int32, device=dev)
-        need = self.workspace_bytes(ld, max_iterations)
-        if self._ws is None or self._ws.numel() < need or self._ws.device != dev:
-            self._ws = torch.empty(need, dtype=torch.uint8, device=dev)
+            iters = torch.empty(B, dtype=torch.int32, device=tdev)
+        check_tensor(final_fi, "final_fi", (self._V, ld), torch.float64, dev)
+        if success.numel() < B or iters.numel() < B:
+            raise ValueError(f"decode_device: success/iters must hold at least B={B} entries")
+        check_tensor(success, "success", (success.numel(),), torch.uint8, dev)
+        check_tensor(iters, "iters", (iters.numel(),), torch.int32, dev)
         if stream is None:
-            stream = torch.cuda.current_stream(dev)
+            stream = torch.cuda.current_stream(tdev)
+        ws = self._workspace(stream, self.workspace_bytes(ld, max_iterations))
         check(_lib.load().qr_decode_batch_device(
             self._h, int(B), int(ld), C.c_void_p(lappr_fi.data_ptr()), C.c_void_p(synd_fi.data_ptr()),
             int(max_iterations), C.c_void_p(final_fi.data_ptr()), C.c_void_p(success.data_ptr()),
-            C.c_void_p(iters.data_ptr()), C.c_void_p(self._ws.data_ptr()), self._ws.numel(),
+            C.c_void_p(iters.data_ptr()), C.c_void_p(ws.data_ptr()), ws.numel(),
             C.c_void_p(stream.cuda_stream)), "decode_device")
         return final_fi, success, iters
+
+    def _workspace(self, stream, need: int):
+        """Device workspace (c2v messages, flags) of the decodes issued on `stream`.
+        Allocated on that stream, so torch's caching allocator orders its reuse after
+        the work queued there; one per stream, so concurrent decodes never race."""
+        import torch
+
+        key = int(stream.cuda_stream)
+        ws = self._ws.get(key)
+        if ws is None or ws.numel() < need:
+            self._ws.pop(key, None)
+            with torch.cuda.stream(stream):
+                ws = torch.empty(need, dtype=torch.uint8, device=torch.device("cuda", self._device))
+            self._ws[key] = ws
+        return ws

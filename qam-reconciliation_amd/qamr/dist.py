@@ -22,23 +22,54 @@ def env_world():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def init(backend: str | None = None):
-    """Initialise torch.distributed when WORLD_SIZE > 1; returns (world, rank, local)."""
+def init(backend: str | None = None, device: int | None = None):
+    """Initialise torch.distributed when WORLD_SIZE > 1; returns (world, rank, local).
+
+    ``backend``: "nccl" (= RCCL on ROCm; one GPU per rank), "gloo" (CPU tensors;
+    the CPU tests and the several-ranks-on-one-GPU rehearsal) or None (RCCL when a
+    GPU is visible).  ``device``: the GPU this rank binds (default: LOCAL_RANK).
+    The world size returned is the one the process group reports."""
     world, rank, local = env_world()
     if world > 1:
         import torch
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dev = local if device is None else int(device)
         if not dist.is_initialized():
             if backend is None:
                 backend = "nccl" if torch.cuda.is_available() else "gloo"
             if backend == "nccl":
-                torch.cuda.set_device(local)
-                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+                torch.cuda.set_device(dev)
+                dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
             else:
                 dist.init_process_group(backend)
+        world, rank = dist.get_world_size(), dist.get_rank()
     return world, rank, local
+
+
+def backend():
+    """The initialised backend name, or None for a single process."""
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_backend()
+    return None
+
+
+def _all_reduce(t, op):
+    """All-reduce in place; under gloo a GPU tensor is staged through the host."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return t
+    if dist.get_backend() == "gloo" and t.is_cuda:
+        h = t.cpu()
+        dist.all_reduce(h, op=op)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op)
+    return t
 
 
 def shard(total: int, world: int, rank: int):
@@ -57,17 +88,13 @@ def rank_seed(seed: int, rank: int, batch_index: int) -> int:
 def all_reduce_sum(t):
     import torch.distributed as dist
 
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return t
+    return _all_reduce(t, dist.ReduceOp.SUM)
 
 
 def all_reduce_max(t):
     import torch.distributed as dist
 
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return t
+    return _all_reduce(t, dist.ReduceOp.MAX)
 
 
 def barrier():
@@ -89,3 +116,50 @@ def early_stop(counters, ferr_count_min: int, simulation_loops: int) -> bool:
     and (frames processed - 1) > simulation_loops / 20."""
     frames = int(counters[4])
     return int(counters[1]) >= ferr_count_min and (frames - 1) > simulation_loops / 20
+
+
+def launch_local(nprocs: int, argv, env_extra=None, poll_s: float = 0.2) -> int:
+    """Start ``nprocs`` ranks of ``python argv...`` on this node (torchrun's env contract:
+    RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT)
+    and wait for them.  The caller must not have touched the GPU: the children are
+    fresh processes (no fork/exec of a GPU-initialised process).  If a rank fails the
+    others are terminated (they would otherwise wait in a collective forever).
+    Returns the first non-zero exit code, else 0."""
+    import socket
+    import subprocess
+    import sys
+    import time
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(nprocs):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nprocs), LOCAL_WORLD_SIZE=str(nprocs),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if env_extra:
+            env.update(env_extra)
+        procs.append(subprocess.Popen([sys.executable] + list(argv), env=env))
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    return rc

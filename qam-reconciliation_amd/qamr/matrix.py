@@ -32,7 +32,8 @@ class Matrix:
         if w.size != self.vnum:
             raise ValueError("Size of word does not match number of vnodes")
         dev = torch.device("cuda", self._code.device)
-        wt = torch.from_numpy(w).to(dev).view(-1, 1).expand(-1, 64).contiguous()
+        wt = torch.zeros((self.vnum, 64), dtype=torch.uint8, device=dev)  # one frame: column 0
+        wt[:, 0] = torch.from_numpy(w).to(dev)
         s = self.eval_syndrome_device(wt, 1)
         torch.cuda.synchronize(dev)
         return s[:, 0].cpu().numpy()
@@ -45,9 +46,12 @@ class Matrix:
 
         from . import _lib
 
+        if not isinstance(word_fi, torch.Tensor) or word_fi.dim() != 2:
+            raise ValueError("eval_syndrome_device: word_fi must be a 2-D tensor [V, ld]")
         V, ld = word_fi.shape
-        if V != self.vnum or word_fi.dtype != torch.uint8:
-            raise ValueError("eval_syndrome_device: expected uint8 [V, ld]")
+        if ld % 64 or not 0 < int(B) <= ld:
+            raise ValueError(f"eval_syndrome_device: need ld % 64 == 0 and 0 < B <= ld (B={B}, ld={ld})")
+        _lib.check_tensor(word_fi, "word_fi", (self.vnum, ld), torch.uint8, self._code.device)
         out = torch.empty((self.cnum, ld), dtype=torch.uint8, device=word_fi.device)
         if stream is None:
             stream = torch.cuda.current_stream(word_fi.device)

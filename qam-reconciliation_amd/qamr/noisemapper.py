@@ -21,8 +21,13 @@ import math
 import numpy as np
 
 from . import _lib
-from ._lib import check, ptr
+from ._lib import check, check_tensor, ptr
 from .alphabet import PAMAlphabet
+
+
+def _check_batch(B, ld, what):
+    if ld % 64 or not 0 < int(B) <= ld:
+        raise ValueError(f"{what}: need ld % 64 == 0 and 0 < B <= ld (B={B}, ld={ld})")
 
 
 def host_tables(a, th, p, sigma, bps):
@@ -194,7 +199,8 @@ class NoiseMapper:
         y = np.ascontiguousarray(np.asarray(y, np.float64).ravel())
         S = y.size
         dev = torch.device("cuda", self._device)
-        yt = torch.from_numpy(y).to(dev).view(S, 1).expand(S, 64).contiguous()
+        yt = torch.zeros((S, 64), dtype=torch.float64, device=dev)  # one frame: column 0
+        yt[:, 0] = torch.from_numpy(y).to(dev)
         xh, nh, w = self.bob_map_device(yt, 1)
         torch.cuda.synchronize(dev)
         return xh[:, 0].cpu().numpy(), nh[:, 0].cpu().numpy(), w[:, 0].cpu().numpy()
@@ -213,9 +219,10 @@ class NoiseMapper:
             raise ValueError("Input vectors sizes do not match")
         S = y.size
         dev = torch.device("cuda", self._device)
-        yt = torch.from_numpy(np.ascontiguousarray(y.ravel())).to(dev).view(S, 1).expand(S, 64).contiguous()
-        it = torch.from_numpy(np.ascontiguousarray(idx.ravel().astype(np.int64))).to(dev)
-        it = it.view(S, 1).expand(S, 64).contiguous()
+        yt = torch.zeros((S, 64), dtype=torch.float64, device=dev)  # one frame: column 0
+        yt[:, 0] = torch.from_numpy(np.ascontiguousarray(y.ravel())).to(dev)
+        it = torch.zeros((S, 64), dtype=torch.int64, device=dev)
+        it[:, 0] = torch.from_numpy(np.ascontiguousarray(idx.ravel().astype(np.int64))).to(dev)
         nh = self.map_noise_device(yt, it, 1)
         torch.cuda.synchronize(dev)
         return nh[:, 0].cpu().numpy()
@@ -224,9 +231,12 @@ class NoiseMapper:
         """y_fi float64 [S, ld], index_fi int64 [S, ld] -> n_hat float64 [S, ld]."""
         import torch
 
+        if not isinstance(y_fi, torch.Tensor) or y_fi.dim() != 2:
+            raise ValueError("map_noise_device: y_fi must be a 2-D tensor [S, ld]")
         S, ld = y_fi.shape
-        if index_fi.shape != (S, ld) or y_fi.dtype != torch.float64 or index_fi.dtype != torch.int64:
-            raise ValueError("map_noise_device: expected y float64 [S, ld] and index int64 [S, ld]")
+        _check_batch(B, ld, "map_noise_device")
+        check_tensor(y_fi, "y_fi", (S, ld), torch.float64, self._device)
+        check_tensor(index_fi, "index_fi", (S, ld), torch.int64, self._device)
         nh = torch.empty((S, ld), dtype=torch.float64, device=y_fi.device)
         if stream is None:
             stream = torch.cuda.current_stream(y_fi.device)
@@ -241,11 +251,15 @@ class NoiseMapper:
         (the decoder's frame-innermost input), scaled by alpha."""
         import torch
 
+        if not isinstance(n_fi, torch.Tensor) or n_fi.dim() != 2:
+            raise ValueError("demap_device: n_fi must be a 2-D tensor [S, ld]")
         S, ld = n_fi.shape
-        if j_fi.shape != (S, ld) or n_fi.dtype != torch.float64 or j_fi.dtype != torch.int64:
-            raise ValueError("demap_device: expected n float64 [S, ld] and j int64 [S, ld]")
+        _check_batch(B, ld, "demap_device")
+        check_tensor(n_fi, "n_fi", (S, ld), torch.float64, self._device)
+        check_tensor(j_fi, "j_fi", (S, ld), torch.int64, self._device)
         if out is None:
             out = torch.empty((S * self.bit_per_symbol, ld), dtype=torch.float64, device=n_fi.device)
+        check_tensor(out, "out", (S * self.bit_per_symbol, ld), torch.float64, self._device)
         if stream is None:
             stream = torch.cuda.current_stream(n_fi.device)
         check(_lib.load().qr_demap_batch_device(self._h, int(B), int(ld), int(S), C.c_void_p(n_fi.data_ptr()),
@@ -258,9 +272,11 @@ class NoiseMapper:
         """y_fi float64 [S, ld] -> (x_hat int64 [S, ld], n_hat float64 [S, ld], word uint8 [S*bps, ld])."""
         import torch
 
+        if not isinstance(y_fi, torch.Tensor) or y_fi.dim() != 2:
+            raise ValueError("bob_map_device: y_fi must be a 2-D tensor [S, ld]")
         S, ld = y_fi.shape
-        if y_fi.dtype != torch.float64:
-            raise ValueError("bob_map_device: expected float64 samples")
+        _check_batch(B, ld, "bob_map_device")
+        check_tensor(y_fi, "y_fi", (S, ld), torch.float64, self._device)
         dev = y_fi.device
         xh = torch.empty((S, ld), dtype=torch.int64, device=dev)
         nh = torch.empty((S, ld), dtype=torch.float64, device=dev)

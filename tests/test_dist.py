@@ -79,3 +79,57 @@ def test_early_stop_rule():
     assert not dist.early_stop([0, 99, 0, 0, 1000], 100, 5000)
     assert not dist.early_stop([0, 100, 0, 0, 251], 100, 5000)   # wordcount 250 is not > 250
     assert dist.early_stop([0, 100, 0, 0, 252], 100, 5000)
+
+
+# ---------------------------------------------------------------- bench.py rank body
+BENCH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")
+
+
+def _bench_line(cmd, extra_env=None):
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ, QAMR_BENCH_STUB="1")
+    env.pop("WORLD_SIZE", None)
+    if extra_env:
+        env.update(extra_env)
+    r = subprocess.run([sys.executable] + cmd, env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # only rank 0 prints
+    return json.loads(lines[0])
+
+
+def _check_world2(out):
+    assert out["n_gpus"] == 2
+    assert out["config"]["global_batch"] == 2 * out["config"]["batch_per_gpu"]
+    assert out["config"]["parallelism"] == "dp2" and out["config"]["backend"] == "gloo"
+    B = out["config"]["batch_per_gpu"]
+    # StubWork rank r contributes [10(r+1), r+1, B-r-1, 7(B-r-1), B]: the line carries the sums
+    assert out["counters"] == [10 + 20, 1 + 2, (B - 1) + (B - 2), 7 * ((B - 1) + (B - 2)), 2 * B]
+    # value = frames of all ranks / max-over-ranks timed region
+    assert abs(out["value"] - 2 * B * out["steps"] / (out["ms_per_step"] * out["steps"] / 1e3)) / out["value"] < 1e-2
+
+
+def test_bench_gpus2_self_launch():
+    """`bench.py --gpus 2` with no WORLD_SIZE starts 2 ranks itself (the configs[4]
+    path at N=2), reports the process group's world size and the summed counters."""
+    _check_world2(_bench_line([BENCH, "--gpus", "2", "--steps", "3", "--warmup", "1"]))
+
+
+def test_bench_gpus2_torchrun():
+    """The driver's launch: torch.distributed.run --nproc-per-node 2 bench.py --gpus 2."""
+    out = _bench_line(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                       "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                       BENCH, "--gpus", "2", "--steps", "2", "--warmup", "1"])
+    _check_world2(out)
+
+
+def test_bench_world_size_must_match_gpus():
+    import subprocess
+    import sys
+
+    env = dict(os.environ, QAMR_BENCH_STUB="1", WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "1"], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "must agree" in r.stderr
