@@ -27,6 +27,7 @@
 #include "fastmath.hpp"
 #include "glibc_math.hpp"
 #include "qamr_internal.hpp"
+#include "strict_pack.hpp"
 
 namespace qr {
 
@@ -172,11 +173,30 @@ struct CheckIn {
 // F[i] = bp(F[i-1], m[i]); the backward values B[i] = bp(B[i+1], m[i]) are consumed as
 // they are produced (out_i = bp(F[i-1], B[i+1])): the same operands as
 // decoder.pyx:341-367, one live B instead of D.  Lane byte offset b8 = f * 8.
+// QR_STRICT_PACK (default 1): the strict update runs the two glibc log paths on full
+// wavefronts (strict_pack.hpp); 0: the sequential loops below, log branch per lane.
+#ifndef QR_STRICT_PACK
+#define QR_STRICT_PACK 0
+#endif
+// LDS of the packed strict update: one kPackWaveDoubles buffer per wavefront of a block.
+template <int AR>
+struct PackLds {
+    static constexpr int doubles = (AR == kStrict && QR_STRICT_PACK) ? 4 * kPackWaveDoubles : 1;
+};
+
 template <int AR, int D, bool NT>
 __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m)[D], int base, uint8_t sb, uint32_t b8,
-                                            const typename Arith<AR>::Tab &tab, const typename Arith<AR>::Regs &K) {
+                                            const typename Arith<AR>::Tab &tab, const typename Arith<AR>::Regs &K,
+                                            double *hb = nullptr) {
     const int ld = a.ld;
     const double s = sb ? -1.0 : 1.0;
+    if constexpr (AR == kStrict && QR_STRICT_PACK) {
+        double out[D];
+        check_strict_packed<D>(m, out, hb + (threadIdx.x >> 6) * kPackWaveDoubles, tab, K);
+#pragma unroll
+        for (int i = 0; i < D; ++i) st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), s * out[i]);
+        return;
+    }
     double F[D - 1];
     F[0] = m[0];
 #pragma unroll
@@ -202,7 +222,7 @@ __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m
 // under an empty exec mask), and a frame's result never depends on its wave-mates.
 template <int D, int MODE, bool NT, int AR>
 __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, unsigned by,
-                                            const typename Arith<AR>::Tab &tab) {
+                                            const typename Arith<AR>::Tab &tab, double *hb) {
     const int ft = 1 << a.g.lft;
     const int nsub = 256 >> a.g.lft;
     const int ld = a.ld;
@@ -252,7 +272,7 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
                     check_exact<kFast, D, NT>(a, m, cur.base, cur.sb, b8, tab, Arith<kFast>::Regs{});
                 }
             } else {
-                check_exact<AR, D, NT>(a, m, cur.base, cur.sb, b8, tab, K);
+                check_exact<AR, D, NT>(a, m, cur.base, cur.sb, b8, tab, K, hb);
             }
         }
         if (!more) break;
@@ -297,8 +317,9 @@ template <int D, int MODE, bool NT, int AR>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AR == kStrict ? QR_CHECK_STRICT_WAVES : 1, 8)))
 k_check(CheckArgs a) {
     __shared__ typename Arith<AR>::Tab tab;
+    __shared__ double hb[PackLds<AR>::doubles];
     if (MODE != kParityOnly) stage_tables<AR>(&tab, a);
-    check_block<D, MODE, NT, AR>(a, blockIdx.x, blockIdx.y, tab);
+    check_block<D, MODE, NT, AR>(a, blockIdx.x, blockIdx.y, tab, hb);
 }
 
 template <bool INIT, bool NT>
@@ -338,12 +359,13 @@ template <int D, int MODE, bool NT, int AR>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FusedWaves<AR>::value, 8)))
 k_fused(CheckArgs ca, VarArgs va, unsigned nb_check, unsigned nb_total) {
     __shared__ typename Arith<AR>::Tab tab;
+    __shared__ double hb[PackLds<AR>::doubles];
     const unsigned b = blockIdx.x;
     const unsigned c0 = (unsigned)(((uint64_t)b * nb_check) / nb_total);
     const unsigned c1 = (unsigned)(((uint64_t)(b + 1) * nb_check) / nb_total);
     if (c1 > c0) {  // block-uniform branch
         stage_tables<AR>(&tab, ca);
-        check_block<D, MODE, NT, AR>(ca, c0 % ca.nbx, c0 / ca.nbx, tab);
+        check_block<D, MODE, NT, AR>(ca, c0 % ca.nbx, c0 / ca.nbx, tab, hb);
     } else {
         const unsigned vi = b - c0;
         var_block<false, NT>(va, vi % va.nbx, vi / va.nbx);

@@ -41,10 +41,27 @@ namespace qr {
 // {tail_i, S_i} per exp interval and {invc, logc} per log interval: 4 KiB, staged in LDS.
 // S_i = asdouble(tab[2i+1] + (i << 45)) is 2^(i/128) as glibc rounds it: glibc's
 // sbits = tab[2i+1] + (ki << 45) is asuint64(S_i) + (k << 52) with k = ki >> 7.
+//
+// lk / lc: the log table path specialised to the box-plus domain u in [1 + 0x1.09p-4, 2]
+// (g_log_table).  There the exponent k of e_log.c is a function of the table index i
+// (u in [1.0647, 1.375): k = 0, i in [88, 127]; u in [1.375, 2]: k = 1, i in [0, 80]), so
+// the k-dependent operations fold into the table, exactly:
+//   z * invc            = u * (invc 2^-k)           (scaling by 2^-k is exact)
+//   fma(k, Ln2hi, logc) = w_i                       (precomputed, same rounding)
+//   fma(k, Ln2lo, lo)   = lo + (k ? Ln2lo : +0.0)   (1*x + lo and 0*x + lo, x > 0)
+// lk[j] = {invc_i 2^-k, w_i, k ? Ln2lo : +0.0, 0} stored at j = (i + 48) & 127 =
+// (hx >> 13) & 127 (the index needs no subtraction of e_log.c's OFF: OFF's low 17 bits
+// are zero and OFF >> 13 = 48 mod 128), 32 B per entry: byte offset (hx >> 8) & 0xFE0.
+struct GlibcLogK {
+    double invc, w, c, pad;
+};
 struct GlibcTables {
     double2 ex[128];
     double2 lg[128];
+    GlibcLogK lk[128];
 };
+
+__host__ __device__ constexpr int glibc_log_k_of_index(int i) { return i <= 80 ? 1 : 0; }
 
 inline void build_glibc_tables(GlibcTables *t) {
     for (int i = 0; i < 128; ++i) {
@@ -52,6 +69,12 @@ inline void build_glibc_tables(GlibcTables *t) {
         t->ex[i].y = __builtin_bit_cast(double, kGxTab[2 * i + 1] + ((uint64_t)i << 45));
         t->lg[i].x = kGlTab[2 * i];
         t->lg[i].y = kGlTab[2 * i + 1];
+        const int k = glibc_log_k_of_index(i);
+        GlibcLogK &e = t->lk[(i + 48) & 127];
+        e.invc = k ? kGlTab[2 * i] * 0.5 : kGlTab[2 * i];
+        e.w = __builtin_fma((double)k, kGlLn2hi, kGlTab[2 * i + 1]);
+        e.c = k ? kGlLn2lo : 0.0;
+        e.pad = 0.0;
     }
 }
 
@@ -68,6 +91,17 @@ __host__ __device__ __forceinline__ uint32_t g_lo(double x) { return (uint32_t)_
 __host__ __device__ __forceinline__ double g_make(uint32_t hi, uint32_t lo) {
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
+// hi + (k << 20) as ONE v_lshl_add_u32 (left to itself the compiler rewrites (ki >> 7) << 20
+// into (ki << 13) & mask and the add into a 64-bit add: three instructions)
+__host__ __device__ __forceinline__ uint32_t g_add_exp(uint32_t hi, int k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, 20, %2" : "=v"(r) : "v"(k), "v"(hi));
+    return r;
+#else
+    return hi + ((uint32_t)k << 20);
+#endif
+}
 
 // glibc exp(x) for |x| < 512 (finite; NaN propagates).  The table index and the
 // exponent come from the low word of kd (|ki| < 2^17, so ki << 45 only touches the
@@ -79,7 +113,7 @@ __host__ __device__ __forceinline__ double g_exp(double x, const GlibcTables &T)
     double r = __builtin_fma(kd, kGxNegLn2hiN, x);
     r = __builtin_fma(kd, kGxNegLn2loN, r);
     const double2 e = T.ex[ki & 127u];
-    const double scale = g_make(g_hi(e.y) + ((uint32_t)((int)ki >> 7) << 20), g_lo(e.y));  // sbits
+    const double scale = g_make(g_add_exp(g_hi(e.y), (int)ki >> 7), g_lo(e.y));  // sbits
     const double r2 = r * r;
     const double p23 = __builtin_fma(r, kGxC3, kGxC2);
     const double tr = e.x + r;
@@ -250,11 +284,12 @@ __constant__ static const GlibcTables kGlibcConst = QR_GLIBC_TABLES_INIT;
 #endif
 struct GlibcK {
     double shift = kGxShift, c2 = kGxC2, c4 = kGxC4, a1 = kGlA1, a3 = kGlA3, b1 = kGlB1, b4 = kGlB4, b7 = kGlB7;
+    double two27 = 0x1p27;  // the near-1 split's multiplier (a VOP3 fma has no literal operand)
     __host__ __device__ static GlibcK pinned() {
         GlibcK k;
 #if defined(__HIP_DEVICE_COMPILE__) && QR_PIN_K
         asm volatile("" : "+v"(k.shift), "+v"(k.c2), "+v"(k.c4), "+v"(k.a1));
-        asm volatile("" : "+v"(k.a3), "+v"(k.b1), "+v"(k.b4), "+v"(k.b7));
+        asm volatile("" : "+v"(k.a3), "+v"(k.b1), "+v"(k.b4), "+v"(k.b7), "+v"(k.two27));
 #endif
         return k;
     }
@@ -277,68 +312,90 @@ __host__ __device__ __forceinline__ double g_exp_neg(double x, const GlibcTables
     const double a = __builtin_fma(p23, r2, tr);
     const double r4 = r2 * r2;
     const double tmp = __builtin_fma(r4, p45, a);
-    const double scale = __builtin_ldexp(e.y, (int)ki >> 7);  // exact: the result is normal here
+    // sbits = asuint64(S_i) + (k << 52), k = ki >> 7: the exponent field of the normal S_i 2^k
+    const double scale = g_make(g_add_exp(g_hi(e.y), (int)ki >> 7), g_lo(e.y));
     return __builtin_fma(scale, tmp, scale);
 }
 
 // log(u) for u = 1.0 + exp(-t) in [1, 2] or NaN: g_log with the main path's scaled
 // mantissa z = u 2^-k taken by ldexp (exact; it also carries a NaN through, which
 // the bit arithmetic would not), and without the u == 1 early return (both branches
-// return +0 there).
-__host__ __device__ __forceinline__ double g_log_u(double x, const GlibcTables &T, const GlibcK &K = GlibcK()) {
-    const uint32_t hx = g_hi(x);
-    if (hx < 0x3FF10900u) {  // u in [1, 1 + 0x1.09p-4): the near-1 branch
-        const double r = x - 1.0;
-        double p2 = __builtin_fma(r, kGlB2, K.b1);
-        double p5 = __builtin_fma(r, kGlB5, K.b4);
-        const double r2 = r * r;
-        double p8 = __builtin_fma(r, kGlB8, K.b7);
-        p2 = __builtin_fma(r2, kGlB3, p2);
-        p5 = __builtin_fma(r2, kGlB6, p5);
-        const double r3 = r * r2;
-        p8 = __builtin_fma(r2, kGlB9, p8);
-        p8 = __builtin_fma(r3, kGlB10, p8);
-        p5 = __builtin_fma(p8, r3, p5);
-        const double P = __builtin_fma(p5, r3, p2);
-        const double t = __builtin_fma(r, 0x1p27, r);
-        const double rhi = __builtin_fma(-0x1p27, r, t);
-        const double rhi2 = rhi * rhi;
-        const double rlo = r - rhi;
-        const double hi = __builtin_fma(rhi2, kGlB0, r);
-        const double d = r - hi;
-        const double rr = r + rhi;
-        double lo = __builtin_fma(rhi2, kGlB0, d);
-        const double q = kGlB0 * rlo;
-        lo = __builtin_fma(q, rr, lo);
-        return hi + __builtin_fma(P, r3, lo);
-    }
-    const uint32_t th = hx - 0x3FE60000u;
-    const int k = (int)th >> 20;
-    const double2 c = T.lg[(th >> 13) & 127u];
-    const double z = __builtin_ldexp(x, -k);
-    const double r = __builtin_fma(z, c.x, -1.0);
-    const double kd = (double)k;
-    const double w = __builtin_fma(kd, kGlLn2hi, c.y);
+// return +0 there).  The two branches are written as separate chains:
+//   g_log_near1  -- u in [1, 1 + 0x1.09p-4) (e_log.c "close to 1.0");
+//   g_log_table  -- the {1/c, log c} table path (any other u).
+__host__ __device__ __forceinline__ double g_log_near1(double x, const GlibcK &K) {
+    const double r = x - 1.0;
+    double p2 = __builtin_fma(r, kGlB2, K.b1);
+    double p5 = __builtin_fma(r, kGlB5, K.b4);
+    const double r2 = r * r;
+    double p8 = __builtin_fma(r, kGlB8, K.b7);
+    p2 = __builtin_fma(r2, kGlB3, p2);
+    p5 = __builtin_fma(r2, kGlB6, p5);
+    const double r3 = r * r2;
+    p8 = __builtin_fma(r2, kGlB9, p8);
+    p8 = __builtin_fma(r3, kGlB10, p8);
+    p5 = __builtin_fma(p8, r3, p5);
+    const double P = __builtin_fma(p5, r3, p2);
+    const double t = __builtin_fma(r, K.two27, r);
+    const double rhi = __builtin_fma(-K.two27, r, t);
+    const double rhi2 = rhi * rhi;
+    const double rlo = r - rhi;
+    const double hi = __builtin_fma(rhi2, kGlB0, r);
+    const double d = r - hi;
+    const double rr = r + rhi;
+    double lo = __builtin_fma(rhi2, kGlB0, d);
+    const double q = kGlB0 * rlo;
+    lo = __builtin_fma(q, rr, lo);
+    return hi + __builtin_fma(P, r3, lo);
+}
+// (k folded into the lk / lc tables, see GlibcTables: valid for x in [1 + 0x1.09p-4, 2]
+// and NaN, the box-plus domain of this path)
+__host__ __device__ __forceinline__ double g_log_table(double x, uint32_t hx, const GlibcTables &T,
+                                                       const GlibcK &K) {
+    const GlibcLogK &c = T.lk[(hx >> 13) & 127u];          // entry of i = ((hx - OFF) >> 13) & 127
+    const double r = __builtin_fma(x, c.invc, -1.0);       // = fma(x 2^-k, invc, -1)
+    const double w = c.w;                                  // = fma(k, Ln2hi, logc)
     const double pA = __builtin_fma(r, kGlA2, K.a1);
     const double hi = r + w;
     const double r2 = r * r;
     double lo = w - hi;
     lo = lo + r;
-    lo = __builtin_fma(kd, kGlLn2lo, lo);
+    lo = lo + c.c;                                         // = fma(k, Ln2lo, lo)
     const double r3 = r * r2;
     double pB = __builtin_fma(r, kGlA4, K.a3);
     lo = __builtin_fma(r2, kGlA0, lo);
     pB = __builtin_fma(pB, r2, pA);
     return __builtin_fma(r3, pB, lo) + hi;
 }
+__host__ __device__ __forceinline__ double g_log_u(double x, const GlibcTables &T, const GlibcK &K = GlibcK()) {
+    const uint32_t hx = g_hi(x);
+    if (hx < 0x3FF10900u) return g_log_near1(x, K);  // u in [1, 1 + 0x1.09p-4)
+    return g_log_table(x, hx, T, K);
+}
+// The same bits without divergent control flow: both chains are evaluated and the
+// lane's branch is selected.  Within a wavefront the 64 frames' arguments straddle
+// the near-1 threshold (t = 2.738) almost always, so the branchy version executes
+// both chains anyway -- one after the other, each a serial dependency chain whose
+// table path starts with an LDS read.  As one basic block the two chains (and those
+// of the other h of the box-plus) interleave and hide each other's latency.
+__host__ __device__ __forceinline__ double g_log_u_sel(double x, const GlibcTables &T, const GlibcK &K = GlibcK()) {
+    const uint32_t hx = g_hi(x);
+    const double yn = g_log_near1(x, K);
+    const double yt = g_log_table(x, hx, T, K);
+    return (hx < 0x3FF10900u) ? yn : yt;
+}
 
 // h(t) exactly as the reference evaluates it.  t > 37.5 is moved into
 // [37.5, 37.5 + 2^-15) by replacing its high word (there exp(-t) < 2^-54, so
 // 1.0 + exp(-t) == 1.0 and log(1.0) == 0, exactly what the reference returns for
 // every t >= 36.74, inf included); NaN fails the compare and propagates.
-__host__ __device__ __forceinline__ double h_strict(double t, const GlibcTables &T, const GlibcK &K = GlibcK()) {
-    const double tc = g_make((t > 37.5) ? 0x4042C000u : g_hi(t), g_lo(t));
-    return g_log_u(1.0 + g_exp_neg(-tc, T, K), T, K);
+// The argument may carry a sign: h(|s|) (the box-plus passes a + b and a - b; the abs
+// and the negation fold into the source modifiers of exp's first fmas).
+template <bool SEL = false>
+__host__ __device__ __forceinline__ double h_strict(double s, const GlibcTables &T, const GlibcK &K = GlibcK()) {
+    const double tc = g_make((fabs(s) > 37.5) ? 0x4042C000u : g_hi(s), g_lo(s));
+    const double u = 1.0 + g_exp_neg(-fabs(tc), T, K);
+    return SEL ? g_log_u_sel(u, T, K) : g_log_u(u, T, K);
 }
 
 // decoder.pyx:41-45: (sgn(a)sgn(b) * min + h(|a+b|)) - h(|a-b|), each operation
@@ -349,22 +406,46 @@ __host__ __device__ __forceinline__ double h_strict(double t, const GlibcTables 
 // for zeros, infinities and NaN) so that each call site sees one population (t+ mostly
 // beyond the near-1 threshold t = 2.738 of g_log, t- mostly below) and its waves
 // rarely have to run both branches of g_log.
+// sgn(a) sgn(b) min(|a|, |b|) with the reference's min, (|b| < |a|) ? |b| : |a|
+// (decoder.pyx:41-45), and the sign as the XOR of the operands' sign bits: selects and
+// bit operations instead of fmin (whose IEEE-mode NaN canonicalisation costs two more
+// fp64 instructions) and a multiply.  Zeros and NaN are discussed above.
+__host__ __device__ __forceinline__ double signed_min(double a, double b) {
+    const bool bl = fabs(b) < fabs(a);
+    const uint32_t hm = bl ? g_hi(b) : g_hi(a), lm = bl ? g_lo(b) : g_lo(a);
+    // bit-field insert: magnitude bits of the selected operand, sign of a XOR b
+    return g_make((hm & 0x7FFFFFFFu) | ((g_hi(a) ^ g_hi(b)) & 0x80000000u), lm);
+}
+
+
+
+// QR_STRICT_SEL: h evaluated branch-free (g_log_u_sel); measured slower on MI355X
+// (5.51 vs 5.22 ms per check launch: same fp64 count, +100 selects), so off by default.
 #ifndef QR_STRICT_MAXMIN
-#define QR_STRICT_MAXMIN 1
+#define QR_STRICT_MAXMIN 0
 #endif
-__host__ __device__ __forceinline__ double box_plus_strict(double a, double b, const GlibcTables &T,
-                                                          const GlibcK &K = GlibcK()) {
-    const double m = fmin(fabs(a), fabs(b));
-    const double ab = a * b;
-    const double sm = copysign(m, ab);
+#ifndef QR_STRICT_SEL
+#define QR_STRICT_SEL 0
+#endif
+template <bool SEL>
+__host__ __device__ __forceinline__ double box_plus_strict_t(double a, double b, const GlibcTables &T,
+                                                            const GlibcK &K = GlibcK()) {
+    const double sm = signed_min(a, b);
 #if QR_STRICT_MAXMIN
-    const double hp = h_strict(fabs(a) + fabs(b), T, K);
-    const double hm = h_strict(fabs(fabs(a) - fabs(b)), T, K);
+    const double ab = a * b;
+#endif
+#if QR_STRICT_MAXMIN
+    const double hp = h_strict<SEL>(fabs(a) + fabs(b), T, K);
+    const double hm = h_strict<SEL>(fabs(fabs(a) - fabs(b)), T, K);
     const bool same = !(ab < 0.0);
     return (sm + (same ? hp : hm)) - (same ? hm : hp);
 #else
-    return (sm + h_strict(fabs(a + b), T, K)) - h_strict(fabs(a - b), T, K);
+    return (sm + h_strict<SEL>(a + b, T, K)) - h_strict<SEL>(a - b, T, K);
 #endif
+}
+__host__ __device__ __forceinline__ double box_plus_strict(double a, double b, const GlibcTables &T,
+                                                          const GlibcK &K = GlibcK()) {
+    return box_plus_strict_t<QR_STRICT_SEL != 0>(a, b, T, K);
 }
 
 }  // namespace qr

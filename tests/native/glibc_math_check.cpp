@@ -37,6 +37,13 @@ int main(int argc, char **argv) {
     const long n = argc > 1 ? atol(argv[1]) : 4000000;
     qr::GlibcTables T;
     qr::build_glibc_tables(&T);
+    {  // the generated constant initializer (device __constant__ copy) == the host builder
+        static const qr::GlibcTables init = QR_GLIBC_TABLES_INIT;
+        if (memcmp(&init, &T, sizeof(T)) != 0) {
+            puts("FAIL QR_GLIBC_TABLES_INIT differs from build_glibc_tables");
+            return 1;
+        }
+    }
     std::mt19937_64 g(11);
     std::uniform_real_distribution<double> U(0.0, 1.0);
     Count ce{"exp"}, cl{"log"}, ch{"h"}, cb{"box_plus"};
@@ -80,10 +87,16 @@ int main(int argc, char **argv) {
         cl.check(log(z), qr::g_log(z, T), z);
         cl.check(log(u), qr::g_log_u(u, T), u);
         cl.check(log(v), qr::g_log_u(v, T), v);
+        cl.check(log(u), qr::g_log_u_sel(u, T), u);
+        cl.check(log(v), qr::g_log_u_sel(v, T), v);
     }
     for (double x : {1.0, 2.0, nextafter(1.0, 2.0), nextafter(2.0, 1.0), 1.0 + 0x1.09p-4, nextafter(1.0 + 0x1.09p-4, 1.0)})
+    {
         cl.check(log(x), qr::g_log_u(x, T), x);
-    if (!std::isnan(qr::g_log_u(std::nan(""), T)) || !std::isnan(qr::g_log_u(-std::nan(""), T))) {
+        cl.check(log(x), qr::g_log_u_sel(x, T), x);
+    }
+    if (!std::isnan(qr::g_log_u(std::nan(""), T)) || !std::isnan(qr::g_log_u(-std::nan(""), T)) ||
+        !std::isnan(qr::g_log_u_sel(std::nan(""), T)) || !std::isnan(qr::g_log_u_sel(-std::nan(""), T))) {
         puts("FAIL g_log_u(NaN) not NaN");
         return 1;
     }
@@ -95,9 +108,14 @@ int main(int argc, char **argv) {
     for (long i = 0; i < n; ++i) {
         const double t = (i % 3 == 0) ? 45.0 * U(g) : (i % 3 == 1) ? 3.0 * U(g) : exp2(-60.0 + 66.0 * U(g));
         ch.check(log(1.0 + exp(-t)), qr::h_strict(t, T), t);
+        ch.check(log(1.0 + exp(-t)), qr::h_strict<true>(t, T), t);
+        ch.check(log(1.0 + exp(-t)), qr::h_strict(-t, T), -t);  // h(|s|)
     }
     for (double t : {0.0, 36.0, 36.7, 36.75, 37.0, 40.0, 41.0, 700.0, 1e300, (double)INFINITY, std::nan("")})
+    {
         ch.check(log(1.0 + exp(-t)), qr::h_strict(t, T), t);
+        ch.check(log(1.0 + exp(-t)), qr::h_strict<true>(t, T), t);
+    }
 
     // box-plus: random operands of both signs, mixed magnitudes, zeros, equal magnitudes, inf/NaN
     const double sc[] = {1e-9, 1e-3, 0.3, 2.0, 8.0, 30.0, 200.0, 1e6};
@@ -107,11 +125,15 @@ int main(int argc, char **argv) {
         if ((i & 63) == 2) b = a;
         if ((i & 127) == 3) a = 0.0;
         if ((i & 127) == 4) b = -0.0;
-        cb.check(qr::box_plus(a, b), qr::box_plus_strict(a, b, T), a, b);
+        cb.check(qr::box_plus(a, b), qr::box_plus_strict_t<false>(a, b, T), a, b);
+        cb.check(qr::box_plus(a, b), qr::box_plus_strict_t<true>(a, b, T), a, b);
     }
     const double sp[] = {0.0, -0.0, 1.5, -2.25, 40.0, (double)INFINITY, -(double)INFINITY, std::nan("")};
     for (double a : sp)
-        for (double b : sp) cb.check(qr::box_plus(a, b), qr::box_plus_strict(a, b, T), a, b);
+        for (double b : sp) {
+            cb.check(qr::box_plus(a, b), qr::box_plus_strict_t<false>(a, b, T), a, b);
+            cb.check(qr::box_plus(a, b), qr::box_plus_strict_t<true>(a, b, T), a, b);
+        }
 
     // full-range exp/log (demapper): random bit patterns over every exponent, specials, subnormals
     Count cef{"exp_full"}, clf{"log_full"};
