@@ -176,7 +176,7 @@ struct CheckIn {
 // QR_STRICT_PACK (default 1): the strict update runs the two glibc log paths on full
 // wavefronts (strict_pack.hpp); 0: the sequential loops below, log branch per lane.
 #ifndef QR_STRICT_PACK
-#define QR_STRICT_PACK 0
+#define QR_STRICT_PACK 1
 #endif
 // LDS of the packed strict update: one kPackWaveDoubles buffer per wavefront of a block.
 template <int AR>
@@ -237,6 +237,10 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
     if (ci >= a.n_checks) return;
     uint32_t bad = 0;
     const auto K = Arith<AR>::regs();
+    // The packed strict update needs the registers the prefetched gathers would hold:
+    // with them it runs at 3 waves/SIMD (142 VGPRs) or spills at 4; without, 4 waves and
+    // 4.54 vs 4.96 ms per launch (MI355X, configs[2]).
+    constexpr bool kPrefetch = QR_CHECK_PREFETCH && !(AR == kStrict && QR_STRICT_PACK);
     CheckIn<D, MODE, NT> nx;
     nx.load(a, ci, f);
     for (int j = 0; j < a.g.per; ++j) {
@@ -254,7 +258,7 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
         struct { int base; uint8_t sb; } cur = {nx.base, nx.sb};
         const int64_t cn = ci + nsub;
         const bool more = (j + 1 < a.g.per) && cn < a.n_checks;   // wave-uniform
-        if (QR_CHECK_PREFETCH && more) nx.load(a, cn, f);
+        if (kPrefetch && more) nx.load(a, cn, f);
         if (MODE != kFirst) bad |= (par == 1u) ? 1u : 0u;  // satisfied iff (parity ^ 1) != 0
         if (MODE != kParityOnly) {
             const uint32_t b8 = (uint32_t)f * 8u;
@@ -276,7 +280,7 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
             }
         }
         if (!more) break;
-        if (!QR_CHECK_PREFETCH) nx.load(a, cn, f);
+        if (!kPrefetch) nx.load(a, cn, f);
         ci = cn;
     }
     if (MODE != kFirst && bad && act) a.unsat[f] = 1;  // benign race: every writer stores 1

@@ -21,31 +21,42 @@
 // from the back (ranks from a wave ballot + mbcnt) -- then the wave runs the near-1 path
 // over ceil(nN/64) full slices and the table path over ceil(nT/64), writes the results
 // in place, and each lane reads its own back: NJ + 1 log passes for NJ = 2K arguments
-// per lane instead of 2 NJ.  Every log is still glibc's __log_fma operation for
+// per lane instead of 2 NJ, ~6 VALU of bookkeeping per argument.  Every log is still glibc's __log_fma operation for
 // operation on its own argument (glibc_math.hpp); only WHICH lane evaluates it changes.
 #pragma once
 #include "glibc_math.hpp"
 
 namespace qr {
 
+// LDS pointers by address (32-bit byte addresses in the LDS aperture).
+typedef __attribute__((address_space(3))) double lds_f64;
+
 // Log arguments per lane per round: at most 4 box-plus x 2 h.
 constexpr int kPackMaxJobs = 8;
-// LDS per wavefront: 64 lanes x kPackMaxJobs doubles = 4 KiB.
-constexpr int kPackWaveDoubles = 64 * kPackMaxJobs;
+// LDS per wavefront: 64 lanes x kPackMaxJobs arguments + one slice of slack (below).
+constexpr int kPackWaveDoubles = 64 * kPackMaxJobs + 64;
 
 // round in which the output box-plus O_i (1 <= i <= D-2) becomes computable
 __host__ __device__ constexpr int pack_out_round(int D, int i) {
     return ((i - 1) > (D - 2 - i) ? (i - 1) : (D - 2 - i)) + 1;
 }
 
-// h(t) for NJ (<= kPackMaxJobs, compile-time after unrolling) arguments per lane.
-// wb: this wavefront's LDS buffer (kPackWaveDoubles).
+// h(t) = log(1.0 + exp(-|t|)) for nj (<= kPackMaxJobs; compile-time after unrolling)
+// arguments per lane.  wb: this wavefront's LDS buffer of kPackWaveDoubles = S slots.
+// The near-1 arguments go to slots [0, nN) in job order, the table ones to (S-1-nT, S-1]
+// counted from the top; a pass is one full 64-slot slice read at an immediate offset and
+// written back in place, unguarded: the surplus lanes of the last near slice write into
+// [nN, nN + 64) and those of the last table slice into (S-1-nT-64, S-1-nT], which never
+// reach the other kind's slots because nN + nT <= S - 64.
 __device__ __forceinline__ void h_packed(const double *t, double *h, int nj, double *wb, const GlibcTables &T,
                                          const GlibcK &K) {
+    constexpr int S = kPackWaveDoubles;
     const uint32_t lane = __lane_id();
-    const uint32_t total = 64u * (uint32_t)nj;
-    uint32_t pos[kPackMaxJobs];
-    uint32_t nN = 0;  // wave-uniform: near-1 arguments written so far
+    uint32_t addr[kPackMaxJobs];  // byte address of the argument's slot
+    uint32_t nN = 0;              // wave-uniform: near-1 arguments written so far
+    // element index of slot s: wb0 + s; a table argument's slot is nN + (near lanes below)
+    // + (S-1 - lane) - 64 j, i.e. the near formula plus a per-lane, per-job offset
+    const uint32_t wb0 = (uint32_t)(uintptr_t)(lds_f64 *)wb / 8u;
 #pragma unroll
     for (int j = 0; j < kPackMaxJobs; ++j) {
         if (j >= nj) break;
@@ -53,35 +64,41 @@ __device__ __forceinline__ void h_packed(const double *t, double *h, int nj, dou
         const double u = 1.0 + g_exp_neg(-fabs(tc), T, K);  // h_strict: h(|t|)
         const bool near = g_hi(u) < 0x3FF10900u;  // g_log_u's branch (NaN: table path)
         const uint64_t mk = __ballot(near);
-        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mk, nN));
-        // near: rank among the near arguments; table: from the back, rank among the others
-        pos[j] = near ? below : (total - 1u) - ((uint32_t)j * 64u + lane - below);
-        wb[pos[j]] = u;
+        const uint32_t x = near ? wb0 : wb0 + (uint32_t)(S - 1) - lane - 64u * (uint32_t)j;
+        const uint32_t a = __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, x));
+        addr[j] = (a + nN) << 3;
+        *(lds_f64 *)(uintptr_t)addr[j] = u;
         nN += (uint32_t)__popcll(mk);
     }
+    const uint32_t nT = 64u * (uint32_t)nj - nN;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // near-1 path over [0, nN), table path over [nN, total); slices are full wavefronts
-    // except one of each kind, whose surplus lanes compute on the other kind's argument
-    // and do not write.
-    for (uint32_t p = 0; p < nN; p += 64u) {
-        const uint32_t i = p + lane;
-        const double y = g_log_near1(wb[i], K);
-        if (i < nN) wb[i] = y;
+    // slices: near q at wn[64 q], table q at wt[64 (kPackMaxJobs - q)]; the next slice is
+    // read before the current one is evaluated (slices past the last one are in bounds)
+    double *wn = wb + lane;
+    double *wt = wb + (S - 1 - 64 * kPackMaxJobs) - lane;
+    double cur = wn[0];
+#pragma unroll
+    for (int q = 0; q <= kPackMaxJobs; ++q) {
+        if (64u * (uint32_t)q >= nN) break;  // wave-uniform
+        const double nxt = (q < kPackMaxJobs) ? wn[64 * (q + 1)] : 0.0;
+        wn[64 * q] = g_log_near1(cur, K);
+        cur = nxt;
     }
-    for (int p = (int)total - 64; p + 64 > (int)nN; p -= 64) {
-        const uint32_t i = (uint32_t)p + lane;
-        const double u = wb[i];
-        const double y = g_log_table(u, g_hi(u), T, K);
-        if (i >= nN) wb[i] = y;
+    cur = wt[64 * kPackMaxJobs];
+#pragma unroll
+    for (int q = 0; q <= kPackMaxJobs; ++q) {
+        if (64u * (uint32_t)q >= nT) break;  // wave-uniform
+        const double nxt = (q < kPackMaxJobs) ? wt[64 * (kPackMaxJobs - q - 1)] : 0.0;
+        wt[64 * (kPackMaxJobs - q)] = g_log_table(cur, g_hi(cur), T, K);
+        cur = nxt;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int j = 0; j < kPackMaxJobs; ++j) {
         if (j >= nj) break;
-        h[j] = wb[pos[j]];
+        h[j] = *(const lds_f64 *)(uintptr_t)addr[j];
     }
     // the next round overwrites the buffer: every lane has read its results first
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
