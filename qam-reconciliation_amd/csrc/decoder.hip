@@ -112,6 +112,8 @@ struct CheckArgs {
     const MathTables *gtab;
     const GlibcTables *gglibc;
     double eps_max;      // exp-domain inputs: |m| <= eps_max (<= kEpsMax)
+    double *fb;          // runtime-degree kernel: F scratch of the class (row fb_base)
+    int64_t fb_base;
 };
 
 // One variable sweep over the frame columns [f_off, f_off + ny*ft).
@@ -376,22 +378,18 @@ k_fused(CheckArgs ca, VarArgs va, unsigned nb_check, unsigned nb_total) {
     }
 }
 
-// Runtime-degree fallback for check degrees above the templated range (2..16).
-constexpr int kMaxGenericDeg = 64;
-
-template <int AR>
-__device__ __forceinline__ void check_update_generic(int d, const double *m, double *out, double s,
-                                                     const typename Arith<AR>::Tab &tab) {
-    double F[kMaxGenericDeg], Bk[kMaxGenericDeg];
-    F[0] = m[0];
-    const auto K = Arith<AR>::regs();
-    for (int i = 1; i < d - 1; ++i) F[i] = Arith<AR>::bp(F[i - 1], m[i], tab, K);
-    Bk[d - 1] = m[d - 1];
-    for (int i = d - 2; i > 0; --i) Bk[i] = Arith<AR>::bp(Bk[i + 1], m[i], tab, K);
-    out[0] = s * Bk[1];
-    for (int i = 1; i < d - 1; ++i) out[i] = s * Arith<AR>::bp(F[i - 1], Bk[i + 1], tab, K);
-    out[d - 1] = s * F[d - 2];
-}
+// Check degrees above the templated range (2..kMaxTemplDeg) take a runtime-degree kernel
+// with no per-lane arrays, so any degree works (the reference sizes its F/B buffer per
+// check, decoder.pyx:131-141): the forward values F_0..F_{d-3} of the reference's
+// recursion are parked in an HBM scratch laid out like c2v (one row of ld doubles per
+// (check, i), frame-innermost, coalesced), and the backward pass re-reads each v2c =
+// post - c2v(old) before it overwrites that edge's message:
+//   forward  F_0 = m_0, F_i = bp(F_{i-1}, m_i)              (rows i-1 <- F_{i-1})
+//   backward c2v[e_{d-1}] = s F_{d-2}; B = m_{d-1};
+//            for i = d-2..1: c2v[e_i] = s bp(F_{i-1}, B); B = bp(B, m_i)
+//            c2v[e_0] = s B
+// (decoder.pyx:322-369: the same box-plus operands in the same order per output.)
+constexpr int kMaxTemplDeg = 16;
 
 template <int MODE, int AR>
 __global__ void __launch_bounds__(256) k_check_generic(CheckArgs a) {
@@ -403,26 +401,46 @@ __global__ void __launch_bounds__(256) k_check_generic(CheckArgs a) {
     const int f = a.f_off + (int)(blockIdx.y << a.g.lft) + (threadIdx.x & (ft - 1));
     const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> a.g.lft);
     if (!a.active[f]) return;
+    const auto K = Arith<AR>::regs();
     const int64_t c0 = (int64_t)blockIdx.x * a.g.per * nsub + sub;
+    const uint32_t b8 = (uint32_t)f * 8u;
     uint32_t bad = 0;
-    double m[kMaxGenericDeg], out[kMaxGenericDeg];
     for (int j = 0; j < a.g.per; ++j) {
         const int64_t ci = c0 + (int64_t)j * nsub;
         if (ci >= a.n_checks) break;
         const int c = a.checks[ci];
         const int base = a.chk_ptr[c];
         const int d = a.chk_ptr[c + 1] - base;
-        const uint8_t sb = a.synd[(size_t)c * ld + f];
+        const uint8_t sb = *at_byte(row_ptr(a.synd, c, ld), (uint32_t)f);
+        const double s = sb ? -1.0 : 1.0;
         uint32_t par = sb;
-        for (int i = 0; i < d; ++i) {
-            const double p = a.post[(size_t)a.chk_var[base + i] * ld + f];
-            if (MODE != kFirst) par ^= (p < 0.0) ? 1u : 0u;
-            m[i] = (MODE == kNormal) ? p - a.c2v[(size_t)a.chk_edge[base + i] * ld + f] : p;
+        // v2c of edge i (decoder.pyx:296-297; first sweep: c2v == 0), parity of post
+        auto msg = [&](int i, bool count) {
+            const double p = *at_byte(row_ptr(a.post, a.chk_var[base + i], ld), b8);
+            if (count && MODE != kFirst) par ^= (p < 0.0) ? 1u : 0u;
+            return (MODE == kNormal) ? p - *at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8) : p;
+        };
+        if (MODE == kParityOnly) {
+            for (int i = 0; i < d; ++i) (void)msg(i, true);
+            bad |= (par == 1u) ? 1u : 0u;
+            continue;
         }
+        double *fb = a.fb + (size_t)(a.fb_base + ci * (int64_t)(d - 2)) * ld;
+        double F = msg(0, true);
+        for (int i = 1; i <= d - 2; ++i) {
+            *at_byte(fb + (size_t)(i - 1) * ld, b8) = F;  // F_{i-1}
+            F = Arith<AR>::bp(F, msg(i, true), tab, K);
+        }
+        double Bn = msg(d - 1, true);
         if (MODE != kFirst) bad |= (par == 1u) ? 1u : 0u;
-        if (MODE == kParityOnly) continue;
-        check_update_generic<AR>(d, m, out, sb ? -1.0 : 1.0, tab);
-        for (int i = 0; i < d; ++i) a.c2v[(size_t)a.chk_edge[base + i] * ld + f] = out[i];
+        *at_byte(row_ptr(a.c2v, a.chk_edge[base + d - 1], ld), b8) = s * F;  // s F_{d-2}
+        for (int i = d - 2; i >= 1; --i) {
+            const double m = msg(i, false);  // before its edge's message is replaced
+            const double Fi = *at_byte(fb + (size_t)(i - 1) * ld, b8);
+            *at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8) = s * Arith<AR>::bp(Fi, Bn, tab, K);
+            Bn = Arith<AR>::bp(Bn, m, tab, K);
+        }
+        *at_byte(row_ptr(a.c2v, a.chk_edge[base], ld), b8) = s * Bn;
     }
     if (MODE != kFirst && bad) a.unsat[f] = 1;
 }
@@ -460,22 +478,26 @@ struct DecodeWs {
     double *c2v;
     uint8_t *active;
     uint8_t *unsat;  // (max_it + 2) rows of ld flags
+    double *fb;      // F scratch of the runtime-degree classes (fb_rows rows of ld), or null
 };
 
 static size_t ws_bytes(const qr_code *code, int ld, int max_it) {
     const int rows = (max_it > 0 ? max_it : 0) + 2;
     return align_up((size_t)code->E * ld * sizeof(double), 256) + align_up((size_t)ld, 256) +
-           align_up((size_t)rows * ld, 256);
+           align_up((size_t)rows * ld, 256) + align_up((size_t)code->fb_rows * ld * sizeof(double), 256);
 }
 
-static DecodeWs carve(const qr_code *code, int ld, void *base) {
+static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
     DecodeWs w;
     char *p = (char *)base;
+    const int rows = (max_it > 0 ? max_it : 0) + 2;
     w.c2v = (double *)p;
     p += align_up((size_t)code->E * ld * sizeof(double), 256);
     w.active = (uint8_t *)p;
     p += align_up((size_t)ld, 256);
     w.unsat = (uint8_t *)p;
+    p += align_up((size_t)rows * ld, 256);
+    w.fb = code->fb_rows ? (double *)p : nullptr;
     return w;
 }
 
@@ -528,6 +550,8 @@ struct Plan {
         a.gtab = code->d_mtab;
         a.gglibc = code->d_gtab;
         a.eps_max = std::min<double>(g_tune.eps_max.load(), kEpsMax);
+        a.fb = w.fb;
+        a.fb_base = cls.fb_base;
         return a;
     }
     VarArgs var_args(int f0, int f1) const {
@@ -635,7 +659,10 @@ static int launch_fused_nt(const Plan &P, const DegreeClass &cls, uint8_t *unsat
         QR_DEG_SWITCH(cls.degree, QR_CASE, handled)
 #undef QR_CASE
     }
-    if (!handled) return set_error(QR_EUNSUPPORTED, "fused launch needs check degree <= 16");
+    if (!handled) {  // runtime degree: the two sweeps as plain launches (disjoint frame columns)
+        int rc = launch_check_class<MODE, NT>(P, cls, P.post, unsat, cf0, cf1);
+        return rc ? rc : launch_var<false>(P, vf0, vf1);
+    }
     QR_LAUNCH_CHECK();
     return QR_OK;
 }
@@ -792,7 +819,7 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     if (ws_size < ws_bytes(code, ld, max_it))
         return set_error(QR_EVALUE, "decode: workspace too small (%zu < %zu)", ws_size, ws_bytes(code, ld, max_it));
     DeviceGuard dg(code->device);
-    Plan P{code, B, ld, lappr, synd, final_post, success, iters, carve(code, ld, ws_ptr), g_tune.nt.load() != 0, s};
+    Plan P{code, B, ld, lappr, synd, final_post, success, iters, carve(code, ld, max_it, ws_ptr), g_tune.nt.load() != 0, s};
     const int rows = (max_it > 0 ? max_it : 0) + 2;
     int rc;
     QR_HIP(hipMemsetAsync(P.w.unsat, 0, (size_t)rows * ld, s));
@@ -853,6 +880,9 @@ __global__ void k_var_nodes(const int64_t *nodes, int64_t n, const int32_t *var_
     for (int k = var_ptr[v]; k < var_ptr[v + 1]; ++k) v2c[var_edge[k]] = p - c2v[var_edge[k]];
 }
 
+// The node-level surface (process_check_node, decoder.pyx:322-369) for any degree: v2c is
+// a separate input here, so the forward values can be parked in the output slots
+// c2v[e_i] <- F_{i-1} and replaced in the backward pass.
 __global__ void k_check_nodes(const int64_t *nodes, int64_t n, const int32_t *chk_ptr, const int32_t *chk_edge,
                               const uint8_t *synd, double *c2v, const double *v2c, const GlibcTables *gtab) {
     __shared__ GlibcTables tab;
@@ -861,10 +891,21 @@ __global__ void k_check_nodes(const int64_t *nodes, int64_t n, const int32_t *ch
     if (i >= n) return;
     const int64_t c = nodes[i];
     const int base = chk_ptr[c], d = chk_ptr[c + 1] - base;
-    double m[kMaxGenericDeg], out[kMaxGenericDeg];
-    for (int k = 0; k < d; ++k) m[k] = v2c[chk_edge[base + k]];
-    check_update_generic<kStrict>(d, m, out, synd[c] ? -1.0 : 1.0, tab);
-    for (int k = 0; k < d; ++k) c2v[chk_edge[base + k]] = out[k];
+    const double s = synd[c] ? -1.0 : 1.0;
+    const int32_t *e = chk_edge + base;
+    double F = v2c[e[0]];
+    for (int k = 1; k <= d - 2; ++k) {
+        c2v[e[k]] = F;  // F_{k-1}
+        F = box_plus_strict(F, v2c[e[k]], tab);
+    }
+    double Bn = v2c[e[d - 1]];
+    c2v[e[d - 1]] = s * F;
+    for (int k = d - 2; k >= 1; --k) {
+        const double Fk = c2v[e[k]];
+        c2v[e[k]] = s * box_plus_strict(Fk, Bn, tab);
+        Bn = box_plus_strict(Bn, v2c[e[k]], tab);
+    }
+    c2v[e[0]] = s * Bn;
 }
 
 }  // namespace qr
@@ -940,8 +981,6 @@ int qr_code_create(const int64_t *e_to_v, const int64_t *e_to_c, int64_t nv, int
                              "check node %lld has degree %d; degree < 2 is undefined behaviour in the reference "
                              "(decoder.pyx:135-141) and is rejected",
                              (long long)c, d);
-        if (d > kMaxGenericDeg)
-            return set_error(QR_EUNSUPPORTED, "check degree %d exceeds the supported maximum %d", d, kMaxGenericDeg);
         max_dc = std::max(max_dc, d);
         if ((int)by_deg.size() <= d) by_deg.resize(d + 1);
         by_deg[d].push_back((int32_t)c);
@@ -981,6 +1020,10 @@ int qr_code_create(const int64_t *e_to_v, const int64_t *e_to_c, int64_t nv, int
     for (int d = 0; d < (int)by_deg.size(); ++d) {
         if (by_deg[d].empty()) continue;
         DegreeClass cls{d, (int64_t)by_deg[d].size(), nullptr};
+        if (d > kMaxTemplDeg) {
+            cls.fb_base = code->fb_rows;
+            code->fb_rows += cls.n * (d - 2);
+        }
         if ((rc = upload(&cls.d_checks, by_deg[d]))) {
             free_code(code);
             return rc;

@@ -80,6 +80,9 @@ struct DegreeClass {
     int32_t degree;
     int64_t n;
     int32_t *d_checks;  // check ids of this degree, ascending
+    // degree > kMaxTemplDeg (runtime-degree kernel): first row of this class's forward
+    // values in the decode workspace's F scratch (n * (degree - 2) rows of ld doubles)
+    int64_t fb_base = 0;
 };
 
 struct qr_code {
@@ -91,6 +94,7 @@ struct qr_code {
     int32_t *d_chk_ptr = nullptr, *d_chk_edge = nullptr, *d_chk_var = nullptr;
     int32_t *d_var_ptr = nullptr, *d_var_edge = nullptr;
     std::vector<DegreeClass> classes;
+    int64_t fb_rows = 0;  // rows of the F scratch (sum over runtime-degree classes)
     qr::MathTables *d_mtab = nullptr;  // box-plus exp/log tables (fastmath.hpp)
     qr::GlibcTables *d_gtab = nullptr; // strict box-plus: glibc exp/log data (glibc_math.hpp)
     mutable qr::Scratch scratch;
