@@ -28,6 +28,7 @@
 #include "glibc_math.hpp"
 #include "qamr_internal.hpp"
 #include "strict_pack.hpp"
+#include "host_build.hpp"
 
 namespace qr {
 
@@ -944,48 +945,14 @@ int qr_code_create(const int64_t *e_to_v, const int64_t *e_to_c, int64_t nv, int
                    qr_code **out) {
     if (!out) return set_error(QR_EVALUE, "null output handle");
     *out = nullptr;
-    if (nv != nc) return set_error(QR_EVALUE, "Sizes don't match");  // decoder.pyx:96-97
-    const int64_t E = nv;
-    if (E <= 0) return set_error(QR_EVALUE, "empty edge list");
-    if (E >= (int64_t)1 << 31) return set_error(QR_EUNSUPPORTED, "more than 2^31-1 edges");
-    int64_t V = 0, C = 0;
-    for (int64_t e = 0; e < E; ++e) {
-        if (e_to_v[e] < 0 || e_to_c[e] < 0) return set_error(QR_EVALUE, "negative node id at edge %lld", (long long)e);
-        V = std::max(V, e_to_v[e] + 1);
-        C = std::max(C, e_to_c[e] + 1);
-    }
-    if (V >= (int64_t)1 << 31 || C >= (int64_t)1 << 31) return set_error(QR_EUNSUPPORTED, "node ids exceed int32");
-    // Stable counting sort by node id == the ascending scan of __build_table (decoder.pyx:69-87).
-    std::vector<int32_t> chk_ptr(C + 1, 0), var_ptr(V + 1, 0), chk_edge(E), chk_var(E), var_edge(E);
-    for (int64_t e = 0; e < E; ++e) {
-        chk_ptr[e_to_c[e] + 1]++;
-        var_ptr[e_to_v[e] + 1]++;
-    }
-    for (int64_t i = 0; i < C; ++i) chk_ptr[i + 1] += chk_ptr[i];
-    for (int64_t i = 0; i < V; ++i) var_ptr[i + 1] += var_ptr[i];
-    {
-        std::vector<int32_t> fc(chk_ptr.begin(), chk_ptr.end() - 1), fv(var_ptr.begin(), var_ptr.end() - 1);
-        for (int64_t e = 0; e < E; ++e) {
-            const int32_t kc = fc[e_to_c[e]]++;
-            chk_edge[kc] = (int32_t)e;
-            chk_var[kc] = (int32_t)e_to_v[e];  // c_to_v (decoder.pyx:128-129)
-            var_edge[fv[e_to_v[e]]++] = (int32_t)e;
-        }
-    }
-    int32_t max_dc = 0, max_dv = 0;
-    std::vector<std::vector<int32_t>> by_deg;
-    for (int64_t c = 0; c < C; ++c) {
-        const int32_t d = chk_ptr[c + 1] - chk_ptr[c];
-        if (d < 2)
-            return set_error(QR_EVALUE,
-                             "check node %lld has degree %d; degree < 2 is undefined behaviour in the reference "
-                             "(decoder.pyx:135-141) and is rejected",
-                             (long long)c, d);
-        max_dc = std::max(max_dc, d);
-        if ((int)by_deg.size() <= d) by_deg.resize(d + 1);
-        by_deg[d].push_back((int32_t)c);
-    }
-    for (int64_t v = 0; v < V; ++v) max_dv = std::max(max_dv, var_ptr[v + 1] - var_ptr[v]);
+    TannerCsr T;  // host_build.hpp (decoder.pyx:60-146)
+    std::string err;
+    if (int rc = build_tanner_csr(e_to_v, e_to_c, nv, nc, T, err)) return set_error(rc, "%s", err.c_str());
+    const int64_t E = T.E, V = T.V, C = T.C;
+    const int32_t max_dc = T.max_dc, max_dv = T.max_dv;
+    std::vector<int32_t> &chk_ptr = T.chk_ptr, &chk_edge = T.chk_edge, &chk_var = T.chk_var, &var_ptr = T.var_ptr,
+                         &var_edge = T.var_edge;
+    std::vector<std::vector<int32_t>> &by_deg = T.by_deg;
 
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)

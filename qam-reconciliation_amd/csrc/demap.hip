@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "qamr_internal.hpp"
+#include "host_build.hpp"
 
 namespace qr {
 
@@ -261,53 +262,19 @@ int qr_demap_create(int32_t bps, const double *constellation, const double *prob
                     double noise_var, const uint8_t *sign_config, int32_t device, qr_demap **out) {
     if (!out) return set_error(QR_EVALUE, "null output handle");
     *out = nullptr;
-    if (bps < 1 || bps > kMaxBps) return set_error(QR_EVALUE, "bit_per_symbol must be in [1, %d], got %d", kMaxBps, bps);
-    // noisemapper.pyx:111-112
-    if (!(noise_var > 0)) return set_error(QR_EVALUE, "noise variance must be strictly positive, got %g", noise_var);
-    if (!constellation || !thresholds) return set_error(QR_EVALUE, "null constellation/thresholds");
+    DemapTables t;  // host_build.hpp (noisemapper.pyx:103-236 + the fast search's tables)
+    std::vector<double2> quant;
+    std::vector<double> ftab;
+    std::string err;
+    if (int rc = build_demap_host(bps, constellation, probabilities, thresholds, noise_var, sign_config, t, quant, ftab,
+                                  err))
+        return set_error(rc, "%s", err.c_str());
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
         return set_error(QR_EDEVICE, "no HIP device available (libqamr has no CPU fallback)");
     if (device < 0 || device >= ndev) return set_error(QR_EVALUE, "device %d out of range", device);
     qr_demap *dm = new qr_demap();
-    DemapTables &t = dm->h;
-    memset(&t, 0, sizeof t);
-    const int M = 1 << bps;
-    t.M = M;
-    t.bps = bps;
-    for (int i = 0; i < M; ++i) {
-        t.a[i] = constellation[i];
-        t.p[i] = probabilities ? probabilities[i] : 1.0 / M;  // alphabet.pyx:46-47
-        t.sign[i] = sign_config ? sign_config[i] : 0;       // noisemapper.pyx:115-116
-    }
-    for (int i = 0; i <= M; ++i) t.thr[i] = thresholds[i];
-    const double sigma = sqrt(noise_var);                     // noisemapper.pyx:132
-    t.den = sqrt(2.0) * sigma;                                // __sqrt2 * sigma (:24, :67)
-    t.two_s2 = 2 * noise_var;                                 // :469
-    t.Fthr[0] = 0;                                            // :149-153
-    t.Fthr[M] = 1;
-    for (int i = 1; i < M; ++i) t.Fthr[i] = single_F_Y(t, t.thr[i]);
-    for (int i = 0; i < M; ++i) t.dF[i] = t.Fthr[i + 1] - t.Fthr[i];  // :159-162
-    t.inv_den = 1.0 / t.den;
-    t.amin = t.amax = t.a[0];
-    for (int i = 1; i < M; ++i) { t.amin = fmin(t.amin, t.a[i]); t.amax = fmax(t.amax, t.a[i]); }
-    // Newton start table (qamr_math.hpp, build_quantiles): M * kQStride * M exact F_Y
-    // bisections; beyond 32-PAM its cost grows as M^2 and the brute search is used.
-    std::vector<double2> quant;
-    if (M <= 32) {
-        quant.resize((size_t)M * kQStride);
-        build_quantiles(t, quant.data());
-    }
-    // Taylor table of F_Y for the Newton evaluation (qamr_math.hpp, build_ftab)
-    std::vector<double> ftab;
-    double ftab_w = 0;
-    if (!quant.empty() && build_ftab(t, ftab, t.ftab_n, t.ftab_lo, ftab_w, t.ftab_err)) {
-        t.ftab_inv_w = 1.0 / ftab_w;
-        t.ftab_h = ftab_w / 2;
-        t.ftab_inv_h = 2.0 / ftab_w;
-    } else {
-        ftab.clear();
-    }
+    dm->h = t;
     std::vector<MathTables> mt(1);
     build_math_tables(&mt[0]);
     dm->device = device;
