@@ -17,7 +17,7 @@
  * the reference through the Python C-API at noisemapper.pyx:66-67) is the
  * cephes algorithm of scipy 1.15.3 (xsf/cephes/ndtr.h): it is restated in
  * orc_erf() below and pinned bit-exactly against scipy by
- * tests/test_oracle_golden.py.
+ * tests/test_oracle.py (scipy erf points stored in tests/golden/demap.npz).
  *
  * Parity pinning: see DESIGN.md "Oracle".  The restatement is checked
  * against golden vectors produced by the reference itself (built from its
