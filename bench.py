@@ -310,13 +310,20 @@ def roofline(args, w, kstats, dev):
                 traffic = t.get("hbm_bytes_per_launch")
                 if t.get("valu_insts_per_launch"):
                     n_all, n64 = t["valu_insts_per_launch"], t.get("valu_f64_insts_per_launch", 0)
-                    busy = (4 * n64 + 2 * (n_all - n64)) / SIMDS / CLOCK_HZ  # s of SIMD issue time
+                    # every wave64 VALU instruction (fp64 or 32-bit) holds its SIMD for one
+                    # quad-cycle in this kernel (SQ_ACTIVE_INST_VALU == SQ_INSTS_VALU)
+                    clk = t.get("clock_ghz_pmc") or CLOCK_HZ / 1e9
+                    busy = 4 * n_all / SIMDS / (clk * 1e9)  # s of SIMD issue time
                     valu = {"wave_insts_per_launch": int(n_all), "f64_wave_insts_per_launch": int(n64),
-                            "issue_ms_at_2.4GHz": round(busy * 1e3, 3),
+                            "clock_ghz": round(clk, 3),
+                            "issue_ms": round(busy * 1e3, 3),
                             "frac": round(busy / avg_s, 4),
+                            "busy_pmc": round(t["valu_busy_pmc"], 4) if t.get("valu_busy_pmc") else None,
                             "source": t.get("source"),
-                            "note": "SIMD issue time of the launch's VALU instructions (f64 4 cyc, "
-                                    "other 2 cyc per wave64) / measured launch time; counts from "
+                            "note": "SIMD issue time of the launch's VALU instructions (4 cycles per wave64 "
+                                    "instruction) at the shader clock measured during the profiled launch "
+                                    "(GRBM_GUI_ACTIVE per XCD / launch time) over the live launch time; "
+                                    "busy_pmc = rocprofv3 VALUBusy of the profiled launch; counts from "
                                     "profiles/pmc_traffic.json (rocprofv3 --pmc)"}
         except Exception:
             traffic = None

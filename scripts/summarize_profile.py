@@ -72,6 +72,16 @@ def main():
                                     "SQ_INSTS_VALU_TRANS_F64") if avg(n) is not None]
             if f64:
                 out["valu_f64_insts_per_launch"] = sum(f64)
+        # VALUBusy as rocprofv3 defines it: SQ_ACTIVE_INST_VALU (quad-cycles, summed over the
+        # SIMDs) / CU_NUM / GRBM_GUI_ACTIVE (per XCD); every wave64 VALU instruction -- fp64
+        # or 32-bit -- occupies one quad-cycle of its SIMD here.  The shader clock during the
+        # launch = GRBM_GUI_ACTIVE per XCD / the traced launch time.
+        xcds, cus = 8, 256
+        if avg("SQ_ACTIVE_INST_VALU") and avg("GRBM_GUI_ACTIVE"):
+            grbm_xcd = avg("GRBM_GUI_ACTIVE") / xcds
+            out["valu_busy_pmc"] = avg("SQ_ACTIVE_INST_VALU") / cus / grbm_xcd
+            if avg_ns.get(args.kernel):
+                out["clock_ghz_pmc"] = grbm_xcd / avg_ns[args.kernel]
         json.dump(out, open(os.path.join(d, "pmc_traffic.json"), "w"), indent=1)
         lines.append(f"\nDominant kernel `{args.kernel}`: HBM traffic per launch "
                      f"{out['hbm_bytes_per_launch'] / 1e9:.2f} GB (2*FETCH + WRITE)")
