@@ -115,6 +115,8 @@ struct CheckArgs {
     double eps_max;      // exp-domain inputs: |m| <= eps_max (<= kEpsMax)
     double *fb;          // runtime-degree kernel: F scratch of the class (row fb_base)
     int64_t fb_base;
+    const int32_t *alist;   // active-frame list (frame ids at alist[f_off + p]) or null
+    const int32_t *acount;  // its length
 };
 
 // One variable sweep over the frame columns [f_off, f_off + ny*ft).
@@ -127,7 +129,26 @@ struct VarArgs {
     int ld, f_off;
     Geom g;
     unsigned nbx;
+    const int32_t *alist, *acount;  // as CheckArgs
 };
+
+// Active-frame compaction (converging operating points, decoder.pyx:431-433: frames stop
+// at their own iteration).  Without a list a sweep's lane p of the frame range is frame
+// f_off + p and stopped frames in a partly stopped wavefront run along; with one (built
+// by k_compact after every status update) lane p is the p-th still-running frame, the
+// range's tail blocks exit at once, and lanes past the count (live = false) repeat the
+// last frame's reads but store nothing (a store would race with that frame's own lane,
+// which may still read the old message).
+__device__ __forceinline__ bool frames_block_live(const int32_t *acount, unsigned by, int lft) {
+    return !acount || (int)(by << lft) < *acount;
+}
+__device__ __forceinline__ int lane_frame(const int32_t *alist, const int32_t *acount, int f_off, int p, bool &live) {
+    live = true;
+    if (!alist) return f_off + p;
+    const int cnt = *acount;
+    live = p < cnt;
+    return alist[f_off + (live ? p : cnt - 1)];
+}
 
 template <int AR>
 __device__ __forceinline__ void stage_tables(typename Arith<AR>::Tab *lds, const CheckArgs &a) {
@@ -190,28 +211,30 @@ struct PackLds {
 template <int AR, int D, bool NT>
 __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m)[D], int base, uint8_t sb, uint32_t b8,
                                             const typename Arith<AR>::Tab &tab, const typename Arith<AR>::Regs &K,
-                                            double *hb = nullptr) {
+                                            double *hb = nullptr, bool live = true) {
     const int ld = a.ld;
     const double s = sb ? -1.0 : 1.0;
     if constexpr (AR == kStrict && QR_STRICT_PACK) {
         double out[D];
         check_strict_packed<D>(m, out, hb + (threadIdx.x >> 6) * kPackWaveDoubles, tab, K);
 #pragma unroll
-        for (int i = 0; i < D; ++i) st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), s * out[i]);
+        for (int i = 0; i < D; ++i)
+            if (live) st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), s * out[i]);
         return;
     }
     double F[D - 1];
     F[0] = m[0];
 #pragma unroll
     for (int i = 1; i < D - 1; ++i) F[i] = Arith<AR>::bp(F[i - 1], m[i], tab, K);
-    st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + D - 1], ld), b8), s * F[D - 2]);
+    if (live) st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + D - 1], ld), b8), s * F[D - 2]);
     double Bn = m[D - 1];
 #pragma unroll
     for (int i = D - 2; i > 0; --i) {
-        st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), s * Arith<AR>::bp(F[i - 1], Bn, tab, K));
+        const double o = s * Arith<AR>::bp(F[i - 1], Bn, tab, K);
+        if (live) st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), o);
         Bn = Arith<AR>::bp(Bn, m[i], tab, K);
     }
-    st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base], ld), b8), s * Bn);
+    if (live) st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base], ld), b8), s * Bn);
 }
 
 // One lane = one (check, frame); each thread walks `per` checks of one degree class.
@@ -229,7 +252,8 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
     const int ft = 1 << a.g.lft;
     const int nsub = 256 >> a.g.lft;
     const int ld = a.ld;
-    const int f = a.f_off + (int)(by << a.g.lft) + (threadIdx.x & (ft - 1));
+    bool live;
+    const int f = lane_frame(a.alist, a.acount, a.f_off, (int)(by << a.g.lft) + (threadIdx.x & (ft - 1)), live);
     const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> a.g.lft);
     // Waves whose 64 frames all stopped leave; in a partly stopped wave the stopped
     // lanes run along (no divergent exit, so the loop state stays scalar): their
@@ -273,20 +297,20 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
                 if (in || !act) {  // stopped lanes never force the exact path
                     const int base = cur.base;
                     check_node_eps<D>(m, cur.sb, tab, [&](int i, double v) {
-                        st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), v);
+                        if (live) st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), v);
                     });
                 } else {
-                    check_exact<kFast, D, NT>(a, m, cur.base, cur.sb, b8, tab, Arith<kFast>::Regs{});
+                    check_exact<kFast, D, NT>(a, m, cur.base, cur.sb, b8, tab, Arith<kFast>::Regs{}, nullptr, live);
                 }
             } else {
-                check_exact<AR, D, NT>(a, m, cur.base, cur.sb, b8, tab, K, hb);
+                check_exact<AR, D, NT>(a, m, cur.base, cur.sb, b8, tab, K, hb, live);
             }
         }
         if (!more) break;
         if (!kPrefetch) nx.load(a, cn, f);
         ci = cn;
     }
-    if (MODE != kFirst && bad && act) a.unsat[f] = 1;  // benign race: every writer stores 1
+    if (MODE != kFirst && bad && act && live) a.unsat[f] = 1;  // benign race: every writer stores 1
 }
 
 // decoder.pyx:285-298: post[v] = lappr[v] + c2v[e_0] + c2v[e_1] + ... (ascending e).
@@ -298,10 +322,11 @@ __device__ __forceinline__ void var_block(const VarArgs &a, unsigned bx, unsigne
     const int ft = 1 << a.g.lft;
     const int nsub = 256 >> a.g.lft;
     const int ld = a.ld;
-    const int f = a.f_off + (int)(by << a.g.lft) + (threadIdx.x & (ft - 1));
+    bool live;
+    const int f = lane_frame(a.alist, a.acount, a.f_off, (int)(by << a.g.lft) + (threadIdx.x & (ft - 1)), live);
     const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> a.g.lft);
     const bool act = a.active[f] != 0;
-    if (!INIT && !act) return;
+    if (!live || (!INIT && !act)) return;
     const int64_t v0 = (int64_t)bx * a.g.per * nsub + sub;
     for (int j = 0; j < a.g.per; ++j) {
         const int64_t v = v0 + (int64_t)j * nsub;
@@ -325,12 +350,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AR == 
 k_check(CheckArgs a) {
     __shared__ typename Arith<AR>::Tab tab;
     __shared__ double hb[PackLds<AR>::doubles];
+    if (!frames_block_live(a.acount, blockIdx.y, a.g.lft)) return;  // block-uniform
     if (MODE != kParityOnly) stage_tables<AR>(&tab, a);
     check_block<D, MODE, NT, AR>(a, blockIdx.x, blockIdx.y, tab, hb);
 }
 
 template <bool INIT, bool NT>
 __global__ void __launch_bounds__(256) k_var(VarArgs a) {
+    if (!frames_block_live(a.acount, blockIdx.y, a.g.lft)) return;
     var_block<INIT, NT>(a, blockIdx.x, blockIdx.y);
 }
 
@@ -371,10 +398,12 @@ k_fused(CheckArgs ca, VarArgs va, unsigned nb_check, unsigned nb_total) {
     const unsigned c0 = (unsigned)(((uint64_t)b * nb_check) / nb_total);
     const unsigned c1 = (unsigned)(((uint64_t)(b + 1) * nb_check) / nb_total);
     if (c1 > c0) {  // block-uniform branch
+        if (!frames_block_live(ca.acount, c0 / ca.nbx, ca.g.lft)) return;
         stage_tables<AR>(&tab, ca);
         check_block<D, MODE, NT, AR>(ca, c0 % ca.nbx, c0 / ca.nbx, tab, hb);
     } else {
         const unsigned vi = b - c0;
+        if (!frames_block_live(va.acount, vi / va.nbx, va.g.lft)) return;
         var_block<false, NT>(va, vi % va.nbx, vi / va.nbx);
     }
 }
@@ -399,9 +428,11 @@ __global__ void __launch_bounds__(256) k_check_generic(CheckArgs a) {
     const int ft = 1 << a.g.lft;
     const int nsub = 256 >> a.g.lft;
     const int ld = a.ld;
-    const int f = a.f_off + (int)(blockIdx.y << a.g.lft) + (threadIdx.x & (ft - 1));
+    if (!frames_block_live(a.acount, blockIdx.y, a.g.lft)) return;
+    bool live;
+    const int f = lane_frame(a.alist, a.acount, a.f_off, (int)(blockIdx.y << a.g.lft) + (threadIdx.x & (ft - 1)), live);
     const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> a.g.lft);
-    if (!a.active[f]) return;
+    if (!live || !a.active[f]) return;
     const auto K = Arith<AR>::regs();
     const int64_t c0 = (int64_t)blockIdx.x * a.g.per * nsub + sub;
     const uint32_t b8 = (uint32_t)f * 8u;
@@ -474,18 +505,47 @@ __global__ void k_status(int f0, int f1, int t, int final_call, int32_t final_it
     }
 }
 
+// The still-running frames of [f0, f1) in ascending order -> list[f0 + 0 .. count).
+// One workgroup of 1024 threads: per 1024-frame chunk a wave ballot, the waves' counts
+// through LDS, one store per running frame.
+__global__ void __launch_bounds__(1024) k_compact(int f0, int f1, const uint8_t *__restrict__ active,
+                                                  int32_t *__restrict__ list, int32_t *__restrict__ count) {
+    __shared__ int wsum[16];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int base = 0;  // running count (every thread keeps the same value)
+    for (int c0 = f0; c0 < f1; c0 += 1024) {
+        const int f = c0 + (int)threadIdx.x;
+        const bool a = f < f1 && active[f];
+        const uint64_t m = __ballot(a);
+        if (lane == 0) wsum[w] = __popcll(m);
+        __syncthreads();
+        int off = base, tot = 0;
+        for (int i = 0; i < 16; ++i) {
+            off += i < w ? wsum[i] : 0;
+            tot += wsum[i];
+        }
+        if (a) list[f0 + off + __popcll(m & ((1ull << lane) - 1ull))] = f;
+        base += tot;
+        __syncthreads();  // wsum is rewritten by the next chunk
+    }
+    if (threadIdx.x == 0) *count = base;
+}
+
 // ------------------------------------------------------------------ launch
 struct DecodeWs {
     double *c2v;
     uint8_t *active;
     uint8_t *unsat;  // (max_it + 2) rows of ld flags
     double *fb;      // F scratch of the runtime-degree classes (fb_rows rows of ld), or null
+    int32_t *alist;  // active-frame lists of the frame ranges (ld entries)
+    int32_t *acount; // their lengths: [0] range starting at frame 0, [1] the second half
 };
 
 static size_t ws_bytes(const qr_code *code, int ld, int max_it) {
     const int rows = (max_it > 0 ? max_it : 0) + 2;
     return align_up((size_t)code->E * ld * sizeof(double), 256) + align_up((size_t)ld, 256) +
-           align_up((size_t)rows * ld, 256) + align_up((size_t)code->fb_rows * ld * sizeof(double), 256);
+           align_up((size_t)rows * ld, 256) + align_up((size_t)code->fb_rows * ld * sizeof(double), 256) +
+           align_up((size_t)ld * sizeof(int32_t), 256) + 256;
 }
 
 static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
@@ -499,13 +559,17 @@ static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
     w.unsat = (uint8_t *)p;
     p += align_up((size_t)rows * ld, 256);
     w.fb = code->fb_rows ? (double *)p : nullptr;
+    p += align_up((size_t)code->fb_rows * ld * sizeof(double), 256);
+    w.alist = (int32_t *)p;
+    p += align_up((size_t)ld * sizeof(int32_t), 256);
+    w.acount = (int32_t *)p;
     return w;
 }
 
 // Runtime tuning knobs (qr_tune_set); defaults picked by scripts/tune.py on MI355X.
 struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3}, math{kStrict}, eps_max{40},
-        lds_pad_kb{0};
+        lds_pad_kb{0}, compact{1};
 };
 static Tuning g_tune;
 
@@ -530,6 +594,9 @@ struct Plan {
     bool nt;
     hipStream_t s;
     int lds_pad = 0;  // dynamic LDS reserved by each check workgroup (caps their CU residency)
+    bool compact = false;  // sweeps of the main loop read the active-frame lists
+
+    const int32_t *count_of(int f0) const { return w.acount + (f0 == 0 ? 0 : 1); }
 
     CheckArgs check_args(const DegreeClass &cls, const double *post_in, uint8_t *unsat, int f0, int f1) const {
         CheckArgs a;
@@ -553,6 +620,7 @@ struct Plan {
         a.eps_max = std::min<double>(g_tune.eps_max.load(), kEpsMax);
         a.fb = w.fb;
         a.fb_base = cls.fb_base;
+        a.alist = a.acount = nullptr;
         return a;
     }
     VarArgs var_args(int f0, int f1) const {
@@ -569,6 +637,7 @@ struct Plan {
         a.g = make_geom(f1 - f0, g_tune.var_ft.load(), g_tune.var_per.load());
         const int64_t per_block = (int64_t)a.g.per * (256 >> a.g.lft);
         a.nbx = (unsigned)((code->V + per_block - 1) / per_block);
+        a.alist = a.acount = nullptr;
         return a;
     }
 };
@@ -590,7 +659,11 @@ static int math_mode(int mode) {
 template <int MODE, bool NT>
 static int launch_check_class(const Plan &P, const DegreeClass &cls, const double *post_in, uint8_t *unsat, int f0,
                               int f1) {
-    const CheckArgs a = P.check_args(cls, post_in, unsat, f0, f1);
+    CheckArgs a = P.check_args(cls, post_in, unsat, f0, f1);
+    if (P.compact && MODE != kParityOnly) {
+        a.alist = P.w.alist;
+        a.acount = P.count_of(f0);
+    }
     const int ar = math_mode(MODE);
     dim3 grid(a.nbx, (unsigned)((f1 - f0) >> a.g.lft));
     ProfScope ps(profiling_on() ? std::string(MODE == kParityOnly ? "parity_d" : MODE == kFirst ? "check1_d" : "check_d") +
@@ -630,7 +703,11 @@ static int launch_checks(const Plan &P, const double *post_in, uint8_t *unsat, i
 template <bool INIT>
 static int launch_var(const Plan &P, int f0, int f1) {
     ProfScope ps(INIT ? "var_init" : "var", P.s);
-    const VarArgs a = P.var_args(f0, f1);
+    VarArgs a = P.var_args(f0, f1);
+    if (P.compact && !INIT) {
+        a.alist = P.w.alist;
+        a.acount = P.count_of(f0);
+    }
     dim3 grid(a.nbx, (unsigned)((f1 - f0) >> a.g.lft));
     if (P.nt) k_var<INIT, true><<<grid, 256, 0, P.s>>>(a);
     else k_var<INIT, false><<<grid, 256, 0, P.s>>>(a);
@@ -640,9 +717,14 @@ static int launch_var(const Plan &P, int f0, int f1) {
 
 template <int MODE, bool NT>
 static int launch_fused_nt(const Plan &P, const DegreeClass &cls, uint8_t *unsat, int cf0, int cf1, int vf0, int vf1) {
-    const CheckArgs ca = P.check_args(cls, P.post, unsat, cf0, cf1);
+    CheckArgs ca = P.check_args(cls, P.post, unsat, cf0, cf1);
     const int ar = math_mode(MODE);
-    const VarArgs va = P.var_args(vf0, vf1);
+    VarArgs va = P.var_args(vf0, vf1);
+    if (P.compact) {
+        ca.alist = va.alist = P.w.alist;
+        ca.acount = P.count_of(cf0);
+        va.acount = P.count_of(vf0);
+    }
     const unsigned nbc = ca.nbx * (unsigned)((cf1 - cf0) >> ca.g.lft);
     const unsigned nbv = va.nbx * (unsigned)((vf1 - vf0) >> va.g.lft);
     bool handled = true;
@@ -685,6 +767,14 @@ static int launch_status(const Plan &P, int f0, int f1, int t, int final_call, i
     return QR_OK;
 }
 
+// Rebuild the active-frame list of [f0, f1) after a status update (no-op without compaction).
+static int launch_compact(const Plan &P, int f0, int f1) {
+    if (!P.compact) return QR_OK;
+    k_compact<<<1, 1024, 0, P.s>>>(f0, f1, P.w.active, P.w.alist, const_cast<int32_t *>(P.count_of(f0)));
+    QR_LAUNCH_CHECK();
+    return QR_OK;
+}
+
 // Flooding schedule, all frames in lock-step (decoder.pyx:424-433).
 static int run_flat(const Plan &P, int max_it) {
     const int ld = P.ld;
@@ -696,6 +786,7 @@ static int run_flat(const Plan &P, int max_it) {
         } else {
             if ((rc = launch_checks<kNormal>(P, P.post, unsat_prev, 0, ld))) return rc;
             if ((rc = launch_status(P, 0, ld, t - 1, 0, 0, unsat_prev))) return rc;
+            if ((rc = launch_compact(P, 0, ld))) return rc;
         }
         if ((rc = launch_var<false>(P, 0, ld))) return rc;
     }
@@ -728,12 +819,14 @@ static int run_split(const Plan &P, int max_it) {
             if ((rc = launch_checks<kNormal>(P, P.post, row(t - 1), B0, B1, big))) return rc;
             if ((rc = launch_fused<kNormal>(P, cls, row(t - 1), B0, B1, A0, A1))) return rc;
             if ((rc = launch_status(P, B0, B1, t - 1, 0, 0, row(t - 1)))) return rc;
+            if ((rc = launch_compact(P, B0, B1))) return rc;
         }
         if (t < max_it) {
             // [C_A(t+1) | V_B(t)]
             if ((rc = launch_checks<kNormal>(P, P.post, row(t), A0, A1, big))) return rc;
             if ((rc = launch_fused<kNormal>(P, cls, row(t), A0, A1, B0, B1))) return rc;
             if ((rc = launch_status(P, A0, A1, t, 0, 0, row(t)))) return rc;
+            if ((rc = launch_compact(P, A0, A1))) return rc;
         } else {
             if ((rc = launch_var<false>(P, B0, B1))) return rc;
         }
@@ -792,12 +885,14 @@ static int run_split2(const Plan &P, int max_it) {
             QR_HIP(hipStreamWaitEvent(P.s, vB, 0));
             if ((rc = launch_checks<kNormal>(C, P.post, row(t - 1), B0, B1))) return rc;
             if ((rc = launch_status(P, B0, B1, t - 1, 0, 0, row(t - 1)))) return rc;
+            if ((rc = launch_compact(P, B0, B1))) return rc;
         }
         QR_HIP(hipEventRecord(cB, P.s));
         if (t < max_it) {
             QR_HIP(hipStreamWaitEvent(P.s, vA, 0));
             if ((rc = launch_checks<kNormal>(C, P.post, row(t), A0, A1))) return rc;
             if ((rc = launch_status(P, A0, A1, t, 0, 0, row(t)))) return rc;
+            if ((rc = launch_compact(P, A0, A1))) return rc;
             QR_HIP(hipEventRecord(cA, P.s));
         }
         QR_HIP(hipStreamWaitEvent(V.s, cB, 0));
@@ -835,6 +930,13 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     for (const auto &c : code->classes) max_deg = std::max(max_deg, c.degree);
     const int sp = g_tune.split.load();
     const bool split = sp >= 2 && ld % 512 == 0 && max_deg <= 16;
+    // active-frame lists of the ranges the schedule sweeps (after the iteration-0 status)
+    P.compact = g_tune.compact.load() != 0;
+    if (split) {
+        if ((rc = launch_compact(P, 0, ld / 2)) || (rc = launch_compact(P, ld / 2, ld))) return rc;
+    } else if ((rc = launch_compact(P, 0, ld))) {
+        return rc;
+    }
     if ((rc = !split ? run_flat(P, max_it) : sp >= 3 ? run_split2(P, max_it) : run_split(P, max_it))) return rc;
     // Check after the last sweep; then every frame still running stops with (0, max).
     const int tf = max_it > 0 ? max_it : 0;
@@ -1009,7 +1111,7 @@ int qr_tune_set(const char *name, int64_t value) {
                         : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
                         : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
                         : n == "math"     ? &g_tune.math     : n == "lds_pad_kb" ? &g_tune.lds_pad_kb : n == "eps_max"   ? &g_tune.eps_max
-                        : n == "demap_fast" ? &g_demap_fast : nullptr;
+                        : n == "compact" ? &g_tune.compact : n == "demap_fast" ? &g_demap_fast : nullptr;
     if (!k) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     if (value < 0 || value > 4096) return set_error(QR_EVALUE, "tuning value out of range");
     k->store((int)value);
@@ -1022,7 +1124,7 @@ int qr_tune_get(const char *name, int64_t *value) {
                               : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
                               : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
                               : n == "math"     ? &g_tune.math     : n == "lds_pad_kb" ? &g_tune.lds_pad_kb : n == "eps_max"   ? &g_tune.eps_max
-                              : n == "demap_fast" ? &g_demap_fast : nullptr;
+                              : n == "compact" ? &g_tune.compact : n == "demap_fast" ? &g_demap_fast : nullptr;
     if (!k || !value) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     *value = k->load();
     return QR_OK;
