@@ -124,6 +124,7 @@ inline int build_demap_host(int32_t bps, const double *constellation, const doub
     const double sigma = sqrt(noise_var);                     // noisemapper.pyx:132
     t.den = sqrt(2.0) * sigma;                                // __sqrt2 * sigma (:24, :67)
     t.two_s2 = 2 * noise_var;                                 // :469
+    t.inv_two_s2 = 1.0 / t.two_s2;                            // div_two_s2
     t.Fthr[0] = 0;                                            // :149-153
     t.Fthr[M] = 1;
     for (int i = 1; i < M; ++i) t.Fthr[i] = single_F_Y(t, t.thr[i]);

@@ -115,6 +115,7 @@ struct DemapTables {
     int32_t M, bps;
     double den;     // sqrt(2) * sigma   (noisemapper.pyx:24, :67)
     double two_s2;  // 2 * noise_var     (noisemapper.pyx:469)
+    double inv_two_s2;  // RN(1 / two_s2): the k > j LLR exponents' division (div_two_s2)
     double a[kMaxOrder];        // constellation
     double p[kMaxOrder];        // probabilities
     double thr[kMaxOrder + 1];  // decision thresholds
@@ -572,6 +573,20 @@ inline void build_quantiles(const DemapTables &t, double2 *quant) {
     }
 }
 
+// x / two_s2 correctly rounded (noisemapper.pyx:512-515 divides) in three operations:
+// q0 = RN(x y) with y = RN(1/b) is within 1 ulp of x/b, r = x - b q0 is exact (fma), and
+// RN(q0 + r y) is the correctly rounded quotient (Markstein's theorem; no overflow or
+// underflow occurs for these arguments: |x| <= ~1e4, b = 2 sigma^2 > 0 normal), except that
+// x = -0 gives +0 (harmless: the quotient only feeds exp, exp(+-0) = 1).  Pinned on
+// the host against the IEEE division (tests/native/division_check.cpp) and on the GPU by
+// the bit-exact demap tests.  The device's IEEE division is a ~10-instruction sequence
+// (v_div_scale x2, v_rcp, fmas, v_div_fmas, v_div_fixup).
+QR_HD double div_two_s2(const DemapTables &t, double x) {
+    const double q0 = x * t.inv_two_s2;
+    const double r = __builtin_fma(-q0, t.two_s2, x);
+    return __builtin_fma(r, t.inv_two_s2, q0);
+}
+
 // noisemapper.pyx:450-540 for one symbol; out[k] = LAPPR of Gray bit k (LSB first).
 // Note the reference quirk kept on purpose: no /2sigma^2 for k < j (:503-507).
 // BPS (= t.bps) is a template parameter: exact-size accumulators (fewer VGPRs, higher
@@ -603,7 +618,7 @@ QR_HD void demap_symbol(const DemapTables& t, const MathTables& mt, const GlibcT
 #pragma unroll 1
         for (int k = 0; k < M; ++k) {
             const double e = (2 * y - t.a[k] - aj) * (t.a[k] - aj);
-            const double arg = k < j ? e : e / t.two_s2;   // a division for k > j, as :512-515
+            const double arg = k < j ? e : div_two_s2(t, e);   // a division for k > j, as :512-515
             const double term = k == j ? t.p[j] : g_exp_full(arg, gt) * t.p[k];
             s += term;
         }

@@ -26,3 +26,21 @@ def test_fast_search_bit_identical(tmp_path):
     print(run.stdout)
     assert run.returncode == 0, run.stdout
     assert "mismatches=0" in run.stdout
+
+
+def test_llr_exponent_division_bit_identical(tmp_path):
+    """qamr_math.hpp::div_two_s2 (reciprocal + FMA correction) == IEEE x / (2 sigma^2)."""
+    src = os.path.join(ROOT, "tests", "native", "division_check.cpp")
+    exe = str(tmp_path / "division_check")
+    csrc = os.path.join(ROOT, "qam-reconciliation_amd", "csrc")
+    if not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("hipcc unavailable")
+    subprocess.run([sys.executable, os.path.join(csrc, "gen_glibc_tables.py"), str(tmp_path / "glibc_tables.inc")],
+                   check=True)
+    cc = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "-ffp-contract=off", "-std=c++17",
+                         "-I" + csrc, "-I" + str(tmp_path), "-o", exe, src], capture_output=True, text=True)
+    assert cc.returncode == 0, cc.stderr[-2000:]
+    run = subprocess.run([exe, "20000000"], capture_output=True, text=True, timeout=300)
+    print(run.stdout)
+    assert run.returncode == 0, run.stdout
+    assert "mismatches=0" in run.stdout
