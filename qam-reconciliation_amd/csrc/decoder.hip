@@ -202,6 +202,10 @@ struct CheckIn {
 #ifndef QR_STRICT_PACK
 #define QR_STRICT_PACK 1
 #endif
+// Degrees whose round loop the compiler still unrolls fully (above, the packed update's
+// register arrays would be indexed dynamically, i.e. live in scratch): the unpacked strict
+// update runs there.
+constexpr int kPackMaxDeg = 10;
 // LDS of the packed strict update: one kPackWaveDoubles buffer per wavefront of a block.
 template <int AR>
 struct PackLds {
@@ -214,7 +218,7 @@ __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m
                                             double *hb = nullptr, bool live = true) {
     const int ld = a.ld;
     const double s = sb ? -1.0 : 1.0;
-    if constexpr (AR == kStrict && QR_STRICT_PACK) {
+    if constexpr (AR == kStrict && QR_STRICT_PACK && D <= kPackMaxDeg) {
         double out[D];
         check_strict_packed<D>(m, out, hb + (threadIdx.x >> 6) * kPackWaveDoubles, tab, K);
 #pragma unroll
