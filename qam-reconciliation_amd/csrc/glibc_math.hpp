@@ -304,7 +304,11 @@ __host__ __device__ __forceinline__ double g_exp_neg(double x, const GlibcTables
     kd = kd - kGxShift;
     double r = __builtin_fma(kd, kGxNegLn2hiN, x);
     r = __builtin_fma(kd, kGxNegLn2loN, r);
+#ifdef QR_EXPERIMENT_UNIFORM_EXP_IDX  // timing only (wrong results): a conflict-free broadcast read
+    const double2 e = T.ex[__builtin_amdgcn_readfirstlane(ki) & 127u];
+#else
     const double2 e = T.ex[ki & 127u];
+#endif
     const double r2 = r * r;
     const double p23 = __builtin_fma(r, kGxC3, K.c2);
     const double tr = e.x + r;
@@ -352,7 +356,11 @@ __host__ __device__ __forceinline__ double g_log_near1(double x, const GlibcK &K
 // and NaN, the box-plus domain of this path)
 __host__ __device__ __forceinline__ double g_log_table(double x, uint32_t hx, const GlibcTables &T,
                                                        const GlibcK &K) {
+#ifdef QR_EXPERIMENT_UNIFORM_LOG_IDX  // timing only (wrong results)
+    const GlibcLogK &c = T.lk[__builtin_amdgcn_readfirstlane(hx >> 13) & 127u];
+#else
     const GlibcLogK &c = T.lk[(hx >> 13) & 127u];          // entry of i = ((hx - OFF) >> 13) & 127
+#endif
     const double r = __builtin_fma(x, c.invc, -1.0);       // = fma(x 2^-k, invc, -1)
     const double w = c.w;                                  // = fma(k, Ln2hi, logc)
     const double pA = __builtin_fma(r, kGlA2, K.a1);
