@@ -76,6 +76,28 @@ __device__ __forceinline__ void st_msg(double *p, double v) {
     else *p = v;
 }
 
+// Read-only graph data (CSR) at a wave-uniform index through the constant address space:
+// the load becomes a scalar s_load instead of a vector load + v_readfirstlane (the
+// compiler cannot prove the generic pointer is not written by the kernel's own stores).
+template <typename T>
+__device__ __forceinline__ T sld(const T *p) {
+    return *(const __attribute__((address_space(4))) T *)p;
+}
+
+// Message / posterior access of the check sweep through a raw buffer resource built from
+// the (wave-uniform) row pointer in scalar registers: the lane's byte offset goes in the
+// instruction's VGPR offset, so an access costs no VALU (a flat/global access needs a
+// 64-bit v_lshl_add per access here, the compiler hoists base + lane offset and adds the
+// scalar row offset per access).  QR_BUFFER_MSG=0: plain loads/stores.
+#ifndef QR_BUFFER_MSG
+#define QR_BUFFER_MSG 1
+#endif
+typedef unsigned int qr_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const double *rowp, int ld) {
+    // word 3 = 0x00020000: DATA_FORMAT 32 (raw dword access), no swizzle; num_records = row bytes
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(rowp), (short)0, ld * 8, 0x00020000);
+}
+
 // Row `row` (wave-uniform) of a frame-innermost array: the row offset is computed in
 // scalar registers; lanes add their byte offset f * sizeof(T).
 template <typename T>
@@ -86,6 +108,23 @@ __device__ __forceinline__ T *row_ptr(T *base, int row, int ld) {
 template <typename T>
 __device__ __forceinline__ T *at_byte(T *rowp, uint32_t boff) {
     return (T *)((char *)rowp + boff);
+}
+// Load / store of the lane's double in a wave-uniform row (row pointer rowp, ld doubles).
+template <bool NT>
+__device__ __forceinline__ double ld_row(const double *rowp, uint32_t b8, int ld) {
+#if QR_BUFFER_MSG
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(row_rsrc(rowp, ld), b8, 0, NT ? 2 : 0));
+#else
+    return ld_msg<NT>(at_byte(rowp, b8));
+#endif
+}
+template <bool NT>
+__device__ __forceinline__ void st_row(double *rowp, uint32_t b8, int ld, double v) {
+#if QR_BUFFER_MSG
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(qr_u32x2, v), row_rsrc(rowp, ld), b8, 0, NT ? 2 : 0);
+#else
+    st_msg<NT>(at_byte(rowp, b8), v);
+#endif
 }
 
 // Block geometry shared by the check and variable sweeps: 256 threads = `ft`
@@ -176,20 +215,20 @@ struct CheckIn {
     __device__ __forceinline__ void load(const CheckArgs &a, int64_t ci, int f) {
         const int ld = a.ld;
         const uint32_t b8 = (uint32_t)f * 8u;
-        const int cc = a.checks[ci];
-        base = a.chk_ptr[cc];
+        const int cc = sld(a.checks + ci);
+        base = sld(a.chk_ptr + cc);
         sb = *at_byte(row_ptr(a.synd, cc, ld), (uint32_t)f);
 #pragma unroll
         for (int i = 0; i < D; ++i) {
-            p[i] = *at_byte(row_ptr(a.post, a.chk_var[base + i], ld), b8);
-            if (MODE == kNormal && QR_PREFETCH_C) c[i] = ld_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8));
+            p[i] = ld_row<false>(row_ptr(a.post, sld(a.chk_var + base + i), ld), b8, ld);
+            if (MODE == kNormal && QR_PREFETCH_C) c[i] = ld_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), ld), b8, ld);
         }
     }
     __device__ __forceinline__ void load_c(const CheckArgs &a, int f) {
         if (MODE != kNormal || QR_PREFETCH_C) return;
         const uint32_t b8 = (uint32_t)f * 8u;
 #pragma unroll
-        for (int i = 0; i < D; ++i) c[i] = ld_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], a.ld), b8));
+        for (int i = 0; i < D; ++i) c[i] = ld_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), a.ld), b8, a.ld);
     }
 };
 
@@ -223,22 +262,22 @@ __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m
         check_strict_packed<D>(m, out, hb + (threadIdx.x >> 6) * kPackWaveDoubles, tab, K);
 #pragma unroll
         for (int i = 0; i < D; ++i)
-            if (live) st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), s * out[i]);
+            if (live) st_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), ld), b8, ld, s * out[i]);
         return;
     }
     double F[D - 1];
     F[0] = m[0];
 #pragma unroll
     for (int i = 1; i < D - 1; ++i) F[i] = Arith<AR>::bp(F[i - 1], m[i], tab, K);
-    if (live) st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + D - 1], ld), b8), s * F[D - 2]);
+    if (live) st_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + D - 1), ld), b8, ld, s * F[D - 2]);
     double Bn = m[D - 1];
 #pragma unroll
     for (int i = D - 2; i > 0; --i) {
         const double o = s * Arith<AR>::bp(F[i - 1], Bn, tab, K);
-        if (live) st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), o);
+        if (live) st_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), ld), b8, ld, o);
         Bn = Arith<AR>::bp(Bn, m[i], tab, K);
     }
-    if (live) st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base], ld), b8), s * Bn);
+    if (live) st_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base), ld), b8, ld, s * Bn);
 }
 
 // One lane = one (check, frame); each thread walks `per` checks of one degree class.
@@ -301,7 +340,7 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
                 if (in || !act) {  // stopped lanes never force the exact path
                     const int base = cur.base;
                     check_node_eps<D>(m, cur.sb, tab, [&](int i, double v) {
-                        if (live) st_msg<NT>(at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8), v);
+                        if (live) st_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), ld), b8, ld, v);
                     });
                 } else {
                     check_exact<kFast, D, NT>(a, m, cur.base, cur.sb, b8, tab, Arith<kFast>::Regs{}, nullptr, live);
@@ -335,12 +374,12 @@ __device__ __forceinline__ void var_block(const VarArgs &a, unsigned bx, unsigne
     for (int j = 0; j < a.g.per; ++j) {
         const int64_t v = v0 + (int64_t)j * nsub;
         if (v >= a.V) break;
-        const int b = a.var_ptr[v], e = a.var_ptr[v + 1];
+        const int b = sld(a.var_ptr + v), e = sld(a.var_ptr + v + 1);
         double p = ld_msg<NT>(&a.lappr[(size_t)v * ld + f]);
         if (INIT) {
             if (act && e > b) p = p + 0.0;
         } else {
-            for (int k = b; k < e; ++k) p += ld_msg<NT>(&a.c2v[(size_t)a.var_edge[k] * ld + f]);
+            for (int k = b; k < e; ++k) p += ld_msg<NT>(&a.c2v[(size_t)sld(a.var_edge + k) * ld + f]);
         }
         a.post[(size_t)v * ld + f] = p;
     }
@@ -444,17 +483,17 @@ __global__ void __launch_bounds__(256) k_check_generic(CheckArgs a) {
     for (int j = 0; j < a.g.per; ++j) {
         const int64_t ci = c0 + (int64_t)j * nsub;
         if (ci >= a.n_checks) break;
-        const int c = a.checks[ci];
-        const int base = a.chk_ptr[c];
-        const int d = a.chk_ptr[c + 1] - base;
+        const int c = sld(a.checks + ci);
+        const int base = sld(a.chk_ptr + c);
+        const int d = sld(a.chk_ptr + c + 1) - base;
         const uint8_t sb = *at_byte(row_ptr(a.synd, c, ld), (uint32_t)f);
         const double s = sb ? -1.0 : 1.0;
         uint32_t par = sb;
         // v2c of edge i (decoder.pyx:296-297; first sweep: c2v == 0), parity of post
         auto msg = [&](int i, bool count) {
-            const double p = *at_byte(row_ptr(a.post, a.chk_var[base + i], ld), b8);
+            const double p = *at_byte(row_ptr(a.post, sld(a.chk_var + base + i), ld), b8);
             if (count && MODE != kFirst) par ^= (p < 0.0) ? 1u : 0u;
-            return (MODE == kNormal) ? p - *at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8) : p;
+            return (MODE == kNormal) ? p - *at_byte(row_ptr(a.c2v, sld(a.chk_edge + base + i), ld), b8) : p;
         };
         if (MODE == kParityOnly) {
             for (int i = 0; i < d; ++i) (void)msg(i, true);
@@ -469,14 +508,14 @@ __global__ void __launch_bounds__(256) k_check_generic(CheckArgs a) {
         }
         double Bn = msg(d - 1, true);
         if (MODE != kFirst) bad |= (par == 1u) ? 1u : 0u;
-        *at_byte(row_ptr(a.c2v, a.chk_edge[base + d - 1], ld), b8) = s * F;  // s F_{d-2}
+        *at_byte(row_ptr(a.c2v, sld(a.chk_edge + base + d - 1), ld), b8) = s * F;  // s F_{d-2}
         for (int i = d - 2; i >= 1; --i) {
             const double m = msg(i, false);  // before its edge's message is replaced
             const double Fi = *at_byte(fb + (size_t)(i - 1) * ld, b8);
-            *at_byte(row_ptr(a.c2v, a.chk_edge[base + i], ld), b8) = s * Arith<AR>::bp(Fi, Bn, tab, K);
+            *at_byte(row_ptr(a.c2v, sld(a.chk_edge + base + i), ld), b8) = s * Arith<AR>::bp(Fi, Bn, tab, K);
             Bn = Arith<AR>::bp(Bn, m, tab, K);
         }
-        *at_byte(row_ptr(a.c2v, a.chk_edge[base], ld), b8) = s * Bn;
+        *at_byte(row_ptr(a.c2v, sld(a.chk_edge + base), ld), b8) = s * Bn;
     }
     if (MODE != kFirst && bad) a.unsat[f] = 1;
 }
