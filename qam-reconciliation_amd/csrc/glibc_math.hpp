@@ -418,11 +418,20 @@ __host__ __device__ __forceinline__ double h_strict(double s, const GlibcTables 
 // (decoder.pyx:41-45), and the sign as the XOR of the operands' sign bits: selects and
 // bit operations instead of fmin (whose IEEE-mode NaN canonicalisation costs two more
 // fp64 instructions) and a multiply.  Zeros and NaN are discussed above.
+__host__ __device__ __forceinline__ uint32_t g_bfi(uint32_t mask, uint32_t a, uint32_t b) {  // (a & mask) | (b & ~mask)
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(mask), "v"(a), "v"(b));  // the compiler's own: and, and, or
+    return r;
+#else
+    return (a & mask) | (b & ~mask);
+#endif
+}
 __host__ __device__ __forceinline__ double signed_min(double a, double b) {
     const bool bl = fabs(b) < fabs(a);
     const uint32_t hm = bl ? g_hi(b) : g_hi(a), lm = bl ? g_lo(b) : g_lo(a);
     // bit-field insert: magnitude bits of the selected operand, sign of a XOR b
-    return g_make((hm & 0x7FFFFFFFu) | ((g_hi(a) ^ g_hi(b)) & 0x80000000u), lm);
+    return g_make(g_bfi(0x7FFFFFFFu, hm, g_hi(a) ^ g_hi(b)), lm);
 }
 
 
