@@ -26,17 +26,13 @@ class Matrix:
 
     def eval_syndrome(self, word):
         """matrix.pyx:55-60: synd[cid[e]] ^= word[vid[e]]."""
-        import torch
-
         w = _as_buffer(word, np.uint8, "word", "unsigned char")
         if w.size != self.vnum:
             raise ValueError("Size of word does not match number of vnodes")
-        dev = torch.device("cuda", self._code.device)
-        wt = torch.zeros((self.vnum, 64), dtype=torch.uint8, device=dev)  # one frame: column 0
-        wt[:, 0] = torch.from_numpy(w).to(dev)
-        s = self.eval_syndrome_device(wt, 1)
-        torch.cuda.synchronize(dev)
-        return s[:, 0].cpu().numpy()
+        # one frame: lane = check node (the node-level surface, qr_check_word_host): against
+        # an all-zero syndrome each check reports (XOR of its word bytes) ^ 1
+        ok, _ = self._code._check_word_flags(w, np.zeros(self.cnum, np.uint8))
+        return ok ^ np.uint8(1)
 
     def eval_syndrome_device(self, word_fi, B: int, stream=None):
         """word_fi uint8 [V, ld] -> synd uint8 [C, ld]."""

@@ -193,17 +193,23 @@ class NoiseMapper:
         return self.demap_lappr_array(np.array([float(n)]), np.array([int(j)], np.int64))
 
     # ----------------------------------------------- Bob side (GPU, batched)
+    # Single-frame (reference-style) calls: the per-symbol maps are elementwise, so one
+    # frame of S symbols is laid out along the frame axis as ONE symbol row of S "frames"
+    # (ld = S rounded up to 64): S lanes of work instead of 64 columns per symbol.
     def _bob_host(self, y):
         import torch
 
         y = np.ascontiguousarray(np.asarray(y, np.float64).ravel())
         S = y.size
+        ld = max(64, -(-S // 64) * 64)
         dev = torch.device("cuda", self._device)
-        yt = torch.zeros((S, 64), dtype=torch.float64, device=dev)  # one frame: column 0
-        yt[:, 0] = torch.from_numpy(y).to(dev)
-        xh, nh, w = self.bob_map_device(yt, 1)
+        yt = torch.zeros((1, ld), dtype=torch.float64, device=dev)
+        yt[0, :S] = torch.from_numpy(y).to(dev)
+        xh, nh, w = self.bob_map_device(yt, S)
         torch.cuda.synchronize(dev)
-        return xh[:, 0].cpu().numpy(), nh[:, 0].cpu().numpy(), w[:, 0].cpu().numpy()
+        # word rows k = Gray bit k of the row's symbol; symbol s's bits are s * bps + k
+        return (xh[0, :S].cpu().numpy(), nh[0, :S].cpu().numpy(),
+                np.ascontiguousarray(w[:, :S].cpu().numpy().T).ravel())
 
     def hard_decide_index(self, y_samples):
         """noisemapper.pyx:349-359"""
@@ -218,14 +224,15 @@ class NoiseMapper:
         if y.size != idx.size:
             raise ValueError("Input vectors sizes do not match")
         S = y.size
+        ld = max(64, -(-S // 64) * 64)  # one frame along the frame axis (see _bob_host)
         dev = torch.device("cuda", self._device)
-        yt = torch.zeros((S, 64), dtype=torch.float64, device=dev)  # one frame: column 0
-        yt[:, 0] = torch.from_numpy(np.ascontiguousarray(y.ravel())).to(dev)
-        it = torch.zeros((S, 64), dtype=torch.int64, device=dev)
-        it[:, 0] = torch.from_numpy(np.ascontiguousarray(idx.ravel().astype(np.int64))).to(dev)
-        nh = self.map_noise_device(yt, it, 1)
+        yt = torch.zeros((1, ld), dtype=torch.float64, device=dev)
+        yt[0, :S] = torch.from_numpy(np.ascontiguousarray(y.ravel())).to(dev)
+        it = torch.zeros((1, ld), dtype=torch.int64, device=dev)
+        it[0, :S] = torch.from_numpy(np.ascontiguousarray(idx.ravel().astype(np.int64))).to(dev)
+        nh = self.map_noise_device(yt, it, S)
         torch.cuda.synchronize(dev)
-        return nh[:, 0].cpu().numpy()
+        return nh[0, :S].cpu().numpy()
 
     def map_noise_device(self, y_fi, index_fi, B: int, stream=None):
         """y_fi float64 [S, ld], index_fi int64 [S, ld] -> n_hat float64 [S, ld]."""

@@ -41,6 +41,27 @@ def test_bob_side_vs_reference(gpu, key, bps):
     assert np.array_equal(xh, g[f"{key}_xhat"])
     nh = nm.map_noise(g[f"{key}_y"], xh)
     assert_bit_exact(nh, g[f"{key}_nhat"])
+    # the single-frame path lays the frame's symbols along the frame axis: Gray words too
+    _, nh2, word = nm._bob_host(g[f"{key}_y"])
+    assert_bit_exact(nh2, g[f"{key}_nhat"])
+    assert np.array_equal(word, np.asarray(g[f"{key}_word"], np.uint8).ravel())
+
+
+def test_single_frame_syndrome_vs_oracle(gpu):
+    """Matrix.eval_syndrome (matrix.pyx:55-60) for one frame: lane = check node."""
+    import qamr
+    from qamr import codes
+    from qamr.matrix import Matrix
+
+    import oracle as O
+
+    vid, cid = codes.regular_code(1008)
+    mat = Matrix(vid, cid)
+    orc = O.OracleCode(vid, cid)
+    rng = np.random.default_rng(8)
+    for _ in range(3):
+        w = rng.integers(0, 2, 1008).astype(np.uint8)
+        assert np.array_equal(mat.eval_syndrome(w), orc.eval_syndrome(w))
 
 
 def test_demap_device_layout_and_alpha(gpu):
