@@ -156,6 +156,7 @@ struct CheckArgs {
     int64_t fb_base;
     const int32_t *alist;   // active-frame list (frame ids at alist[f_off + p]) or null
     const int32_t *acount;  // its length
+    const int32_t *finite;  // strict arithmetic: 1 iff the batch's input LAPPRs are all finite (or null)
 };
 
 // One variable sweep over the frame columns [f_off, f_off + ny*ft).
@@ -245,13 +246,30 @@ struct CheckIn {
 // register arrays would be indexed dynamically, i.e. live in scratch): the unpacked strict
 // update runs there.
 constexpr int kPackMaxDeg = 10;
+// QR_STRICT_FINITE (default 1): when every input LAPPR of the batch's frames is below a bound
+// 2^e (a device flag computed at the start of the decode, k_finite), no inf or NaN can arise
+// in any sweep: |c2v| <= max |v2c| (a box-plus never exceeds its smaller operand, to
+// rounding) and |v2c| <= |L| + (dv - 1) max |c2v|, so X_t = max |post| + max |c2v| after
+// sweep t obeys X_{t+1} <= |L| + (dv + 1) X_t and every value (box-plus arguments, twice
+// that) stays below 2^e (dv + 1)^(max_it + 2), which e = 1000 - (max_it + 2) log2(dv_max + 1)
+// keeps finite.  The check
+// sweeps then run the packed update with the one-instruction clamp (strict_pack.hpp
+// kClampFinite) instead of the NaN-preserving two-instruction one.
+// QR_STRICT_UNCLAMPED (default 0): within those sweeps, waves whose check inputs are all
+// below 350 in magnitude run without any clamp (two code paths in the loop: more VGPRs).
+#ifndef QR_STRICT_FINITE
+#define QR_STRICT_FINITE 1
+#endif
+#ifndef QR_STRICT_UNCLAMPED
+#define QR_STRICT_UNCLAMPED 0
+#endif
 // LDS of the packed strict update: one kPackWaveDoubles buffer per wavefront of a block.
 template <int AR>
 struct PackLds {
     static constexpr int doubles = (AR == kStrict && QR_STRICT_PACK) ? 4 * kPackWaveDoubles : 1;
 };
 
-template <int AR, int D, bool NT>
+template <int AR, int D, bool NT, bool FIN = false>
 __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m)[D], int base, uint8_t sb, uint32_t b8,
                                             const typename Arith<AR>::Tab &tab, const typename Arith<AR>::Regs &K,
                                             double *hb = nullptr, bool live = true) {
@@ -259,7 +277,24 @@ __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m
     const double s = sb ? -1.0 : 1.0;
     if constexpr (AR == kStrict && QR_STRICT_PACK && D <= kPackMaxDeg) {
         double out[D];
-        check_strict_packed<D>(m, out, hb + (threadIdx.x >> 6) * kPackWaveDoubles, tab, K);
+        double *wb = hb + (threadIdx.x >> 6) * kPackWaveDoubles;
+        if constexpr (FIN) {
+#if QR_STRICT_UNCLAMPED
+            // Every h argument of the check is |F +- m|, |B +- m| or |F +- B|, and |F|, |B| <=
+            // max |m_i| (the box-plus magnitude never exceeds min(|a|, |b|), to rounding), so
+            // inputs below 350 keep every argument below 700: the wave runs the update
+            // without a clamp when all its lanes qualify.
+            bool small = true;
+#pragma unroll
+            for (int i = 0; i < D; ++i) small &= __builtin_fabs(m[i]) < 350.0;
+            if (__ballot(!small) == 0) check_strict_packed<D, kClampNone>(m, out, wb, tab, K);
+            else check_strict_packed<D, kClampFinite>(m, out, wb, tab, K);
+#else
+            check_strict_packed<D, kClampFinite>(m, out, wb, tab, K);
+#endif
+        } else {
+            check_strict_packed<D, kClampFull>(m, out, wb, tab, K);
+        }
 #pragma unroll
         for (int i = 0; i < D; ++i)
             if (live) st_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), ld), b8, ld, s * out[i]);
@@ -289,7 +324,7 @@ __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m
 // VALU instructions) in every lane whose inputs are all in its domain, the exact path
 // in the others; a wave whose lanes agree runs one path only (the other is skipped
 // under an empty exec mask), and a frame's result never depends on its wave-mates.
-template <int D, int MODE, bool NT, int AR>
+template <int D, int MODE, bool NT, int AR, bool FIN = false>
 __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, unsigned by,
                                             const typename Arith<AR>::Tab &tab, double *hb) {
     const int ft = 1 << a.g.lft;
@@ -346,7 +381,7 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
                     check_exact<kFast, D, NT>(a, m, cur.base, cur.sb, b8, tab, Arith<kFast>::Regs{}, nullptr, live);
                 }
             } else {
-                check_exact<AR, D, NT>(a, m, cur.base, cur.sb, b8, tab, K, hb, live);
+                check_exact<AR, D, NT, FIN>(a, m, cur.base, cur.sb, b8, tab, K, hb, live);
             }
         }
         if (!more) break;
@@ -395,7 +430,24 @@ k_check(CheckArgs a) {
     __shared__ double hb[PackLds<AR>::doubles];
     if (!frames_block_live(a.acount, blockIdx.y, a.g.lft)) return;  // block-uniform
     if (MODE != kParityOnly) stage_tables<AR>(&tab, a);
+    if constexpr (AR == kStrict && MODE != kParityOnly && QR_STRICT_FINITE && QR_STRICT_PACK && D <= kPackMaxDeg) {
+        if (a.finite && sld(a.finite)) {  // kernel-uniform: one of the two bodies runs
+            check_block<D, MODE, NT, AR, true>(a, blockIdx.x, blockIdx.y, tab, hb);
+            return;
+        }
+    }
     check_block<D, MODE, NT, AR>(a, blockIdx.x, blockIdx.y, tab, hb);
+}
+
+// finite = 1 iff every LAPPR of frames [0, B) is below bound in magnitude (the flag was set
+// to 1 by k_init_status; every thread that sees a larger, infinite or NaN value stores 0).
+__global__ void __launch_bounds__(256) k_finite(const double *__restrict__ lappr, int64_t V, int ld, int B,
+                                                double bound, int32_t *finite) {
+    bool bad = false;
+    for (int64_t r = blockIdx.y; r < V; r += gridDim.y)
+        for (int f = blockIdx.x * 256 + threadIdx.x; f < B; f += gridDim.x * 256)
+            bad |= !(__builtin_fabs(lappr[r * ld + f]) < bound);
+    if (bad) *finite = 0;
 }
 
 template <bool INIT, bool NT>
@@ -520,8 +572,9 @@ __global__ void __launch_bounds__(256) k_check_generic(CheckArgs a) {
     if (MODE != kFirst && bad) a.unsat[f] = 1;
 }
 
-__global__ void k_init_status(int B, int ld, uint8_t *active, uint8_t *success, int32_t *iters) {
+__global__ void k_init_status(int B, int ld, uint8_t *active, uint8_t *success, int32_t *iters, int32_t *finite) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f == 0) *finite = 1;
     if (f >= ld) return;
     active[f] = (f < B) ? 1 : 0;
     if (f < B) {
@@ -581,7 +634,8 @@ struct DecodeWs {
     uint8_t *unsat;  // (max_it + 2) rows of ld flags
     double *fb;      // F scratch of the runtime-degree classes (fb_rows rows of ld), or null
     int32_t *alist;  // active-frame lists of the frame ranges (ld entries)
-    int32_t *acount; // their lengths: [0] range starting at frame 0, [1] the second half
+    int32_t *acount; // their lengths: [0] range starting at frame 0, [1] the second half;
+                     // [2] the finite flag of the input LAPPRs (k_finite)
 };
 
 static size_t ws_bytes(const qr_code *code, int ld, int max_it) {
@@ -664,6 +718,7 @@ struct Plan {
         a.fb = w.fb;
         a.fb_base = cls.fb_base;
         a.alist = a.acount = nullptr;
+        a.finite = w.acount + 2;
         return a;
     }
     VarArgs var_args(int f0, int f1) const {
@@ -962,8 +1017,18 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     const int rows = (max_it > 0 ? max_it : 0) + 2;
     int rc;
     QR_HIP(hipMemsetAsync(P.w.unsat, 0, (size_t)rows * ld, s));
-    k_init_status<<<(ld + 255) / 256, 256, 0, s>>>(B, ld, P.w.active, success, iters);
+    k_init_status<<<(ld + 255) / 256, 256, 0, s>>>(B, ld, P.w.active, success, iters, P.w.acount + 2);
     QR_LAUNCH_CHECK();
+    // the finite flag (QR_STRICT_FINITE): bound 2^e with e = 1000 - (max_it + 2) log2(dv_max + 1)
+    const int fin_e = 1000 - (int)std::ceil((std::max(max_it, 0) + 2) * std::log2((double)code->max_dv + 1.0));
+    if (fin_e < 1) {
+        QR_HIP(hipMemsetAsync(P.w.acount + 2, 0, sizeof(int32_t), s));
+    } else if (g_tune.math.load() == kStrict) {
+        const unsigned gx = (unsigned)std::min(16, (B + 255) / 256);
+        k_finite<<<dim3(gx, (unsigned)std::min<int64_t>(code->V, 4096 / gx)), 256, 0, s>>>(
+            lappr, code->V, ld, B, std::ldexp(1.0, fin_e), P.w.acount + 2);
+        QR_LAUNCH_CHECK();
+    }
     // decoder.pyx:400-405: the input itself may already satisfy the syndrome.
     if ((rc = launch_checks<kParityOnly>(P, lappr, P.w.unsat, 0, ld))) return rc;
     if ((rc = launch_status(P, 0, ld, 0, 0, 0, P.w.unsat))) return rc;

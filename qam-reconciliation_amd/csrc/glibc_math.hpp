@@ -38,9 +38,10 @@
 
 namespace qr {
 
-// {tail_i, S_i} per exp interval and {invc, logc} per log interval: 4 KiB, staged in LDS.
-// S_i = asdouble(tab[2i+1] + (i << 45)) is 2^(i/128) as glibc rounds it: glibc's
-// sbits = tab[2i+1] + (ki << 45) is asuint64(S_i) + (k << 52) with k = ki >> 7.
+// {tail_i, tab[2i+1]} per exp interval and {invc, logc} per log interval, staged in LDS.
+// glibc's sbits = tab[2i+1] + (ki << 45) (e_exp.c): only the high word changes, by
+// ki << 13 (mod 2^32; the low 19 bits of ki, i.e. the low word of kd), so the scale's
+// high word is ONE v_lshl_add_u32 (ki, 13, hi(tab[2i+1])) -- no separate k = ki >> 7.
 //
 // lk / lc: the log table path specialised to the box-plus domain u in [1 + 0x1.09p-4, 2]
 // (g_log_table).  There the exponent k of e_log.c is a function of the table index i
@@ -66,7 +67,7 @@ __host__ __device__ constexpr int glibc_log_k_of_index(int i) { return i <= 80 ?
 inline void build_glibc_tables(GlibcTables *t) {
     for (int i = 0; i < 128; ++i) {
         t->ex[i].x = __builtin_bit_cast(double, kGxTab[2 * i]);
-        t->ex[i].y = __builtin_bit_cast(double, kGxTab[2 * i + 1] + ((uint64_t)i << 45));
+        t->ex[i].y = __builtin_bit_cast(double, kGxTab[2 * i + 1]);
         t->lg[i].x = kGlTab[2 * i];
         t->lg[i].y = kGlTab[2 * i + 1];
         const int k = glibc_log_k_of_index(i);
@@ -91,15 +92,15 @@ __host__ __device__ __forceinline__ uint32_t g_lo(double x) { return (uint32_t)_
 __host__ __device__ __forceinline__ double g_make(uint32_t hi, uint32_t lo) {
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
-// hi + (k << 20) as ONE v_lshl_add_u32 (left to itself the compiler rewrites (ki >> 7) << 20
-// into (ki << 13) & mask and the add into a 64-bit add: three instructions)
-__host__ __device__ __forceinline__ uint32_t g_add_exp(uint32_t hi, int k) {
+// high word of glibc's sbits = tab[2i+1] + (ki << 45): hi + (ki << 13) as ONE v_lshl_add_u32
+// (left to itself the compiler turns the shift-add into a 64-bit add)
+__host__ __device__ __forceinline__ uint32_t g_add_ki(uint32_t hi, uint32_t ki) {
 #if defined(__HIP_DEVICE_COMPILE__)
     uint32_t r;
-    asm("v_lshl_add_u32 %0, %1, 20, %2" : "=v"(r) : "v"(k), "v"(hi));
+    asm("v_lshl_add_u32 %0, %1, 13, %2" : "=v"(r) : "v"(ki), "v"(hi));
     return r;
 #else
-    return hi + ((uint32_t)k << 20);
+    return hi + (ki << 13);
 #endif
 }
 
@@ -113,7 +114,7 @@ __host__ __device__ __forceinline__ double g_exp(double x, const GlibcTables &T)
     double r = __builtin_fma(kd, kGxNegLn2hiN, x);
     r = __builtin_fma(kd, kGxNegLn2loN, r);
     const double2 e = T.ex[ki & 127u];
-    const double scale = g_make(g_add_exp(g_hi(e.y), (int)ki >> 7), g_lo(e.y));  // sbits
+    const double scale = g_make(g_add_ki(g_hi(e.y), ki), g_lo(e.y));  // sbits
     const double r2 = r * r;
     const double p23 = __builtin_fma(r, kGxC3, kGxC2);
     const double tr = e.x + r;
@@ -204,7 +205,7 @@ __host__ __device__ __forceinline__ double g_exp_full(double x, const GlibcTable
     double r = __builtin_fma(kd, kGxNegLn2hiN, x);
     r = __builtin_fma(kd, kGxNegLn2loN, r);
     const double2 e = T.ex[ki & 127u];
-    const uint32_t shi = g_hi(e.y) + ((uint32_t)((int)ki >> 7) << 20), slo = g_lo(e.y);
+    const uint32_t shi = g_add_ki(g_hi(e.y), ki), slo = g_lo(e.y);
     const double r2 = r * r;
     const double p23 = __builtin_fma(r, kGxC3, kGxC2);
     const double tr = e.x + r;
@@ -316,8 +317,8 @@ __host__ __device__ __forceinline__ double g_exp_neg(double x, const GlibcTables
     const double a = __builtin_fma(p23, r2, tr);
     const double r4 = r2 * r2;
     const double tmp = __builtin_fma(r4, p45, a);
-    // sbits = asuint64(S_i) + (k << 52), k = ki >> 7: the exponent field of the normal S_i 2^k
-    const double scale = g_make(g_add_exp(g_hi(e.y), (int)ki >> 7), g_lo(e.y));
+    // sbits = tab[2i+1] + (ki << 45): the normal 2^(i/128) 2^k of glibc
+    const double scale = g_make(g_add_ki(g_hi(e.y), ki), g_lo(e.y));
     return __builtin_fma(scale, tmp, scale);
 }
 

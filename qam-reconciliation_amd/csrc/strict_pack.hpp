@@ -48,6 +48,17 @@ __host__ __device__ constexpr int pack_out_round(int D, int i) {
 // written back in place, unguarded: the surplus lanes of the last near slice write into
 // [nN, nN + 64) and those of the last table slice into (S-1-nT-64, S-1-nT], which never
 // reach the other kind's slots because nN + nT <= S - 64.
+// The argument of exp, -|t|, by clamp mode CL:
+//   kClampFull  : t > 37.5 moved into [37.5, 37.5 + 2^-15) by its high word (h_strict; any
+//                 input, NaN propagates);
+//   kClampFinite: max(-|t|, -700), one v_max_f64 -- for waves whose inputs are all finite,
+//                 where no NaN can arise in the box-plus (finite operands give finite t, h);
+//   kClampNone  : -|t| as it stands -- every |t| < 700 (the caller has checked its inputs).
+// Below 700 glibc exp's main path is valid for -|t| as written (normal result, k >= -1010),
+// and for every t > 37.5 exp(-t) < 2^-54, so u = fl(1.0 + exp(-t)) == 1.0 and h == +0 in all
+// three modes: the same bits.
+enum { kClampNone = 0, kClampFull = 1, kClampFinite = 2 };
+template <int CL = kClampFull>
 __device__ __forceinline__ void h_packed(const double *t, double *h, int nj, double *wb, const GlibcTables &T,
                                          const GlibcK &K) {
     constexpr int S = kPackWaveDoubles;
@@ -60,8 +71,11 @@ __device__ __forceinline__ void h_packed(const double *t, double *h, int nj, dou
 #pragma unroll
     for (int j = 0; j < kPackMaxJobs; ++j) {
         if (j >= nj) break;
-        const double tc = g_make((fabs(t[j]) > 37.5) ? 0x4042C000u : g_hi(t[j]), g_lo(t[j]));
-        const double u = 1.0 + g_exp_neg(-fabs(tc), T, K);  // h_strict: h(|t|)
+        double xe;
+        if constexpr (CL == kClampFull) xe = -fabs(g_make((fabs(t[j]) > 37.5) ? 0x4042C000u : g_hi(t[j]), g_lo(t[j])));
+        else if constexpr (CL == kClampFinite) xe = __builtin_fmax(-fabs(t[j]), -700.0);
+        else xe = -fabs(t[j]);
+        const double u = 1.0 + g_exp_neg(xe, T, K);  // h_strict: h(|t|)
         const bool near = g_hi(u) < 0x3FF10900u;  // g_log_u's branch (NaN: table path)
         const uint64_t mk = __ballot(near);
         const uint32_t x = near ? wb0 : wb0 + (uint32_t)(S - 1) - lane - 64u * (uint32_t)j;
@@ -105,10 +119,27 @@ __device__ __forceinline__ void h_packed(const double *t, double *h, int nj, dou
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// sgn(a) sgn(b) min(|a|, |b|) of the box-plus (decoder.pyx:41-45) with the magnitude from
+// v_min_f64 (QR_STRICT_FMIN, default): every operand here is the result of an fp64 add or
+// subtract, so the compiler knows it canonical and emits one v_min_f64 with |.| modifiers
+// instead of the compare + two selects.  Equal magnitudes have equal bits (+-0 included),
+// and a NaN operand makes both h arguments NaN, so the box-plus is NaN whatever min returns.
+#ifndef QR_STRICT_FMIN
+#define QR_STRICT_FMIN 1
+#endif
+__device__ __forceinline__ double signed_min_packed(double a, double b) {
+#if QR_STRICT_FMIN
+    const double mn = __builtin_fmin(__builtin_fabs(a), __builtin_fabs(b));
+    return g_make(g_bfi(0x7FFFFFFFu, g_hi(mn), g_hi(a) ^ g_hi(b)), g_lo(mn));
+#else
+    return signed_min(a, b);
+#endif
+}
+
 // decoder.pyx:322-369 for one check of degree D (>= 2): out[i] = c2v of edge i before
 // the syndrome sign.  The same box-plus (operands and box_plus_strict's operation order)
 // as check_exact<kStrict>, evaluated round by round.
-template <int D>
+template <int D, int CL = kClampFull>
 __device__ __forceinline__ void check_strict_packed(const double (&m)[D], double (&out)[D], double *wb,
                                                     const GlibcTables &T, const GlibcK &K) {
     if constexpr (D == 2) {
@@ -134,11 +165,11 @@ __device__ __forceinline__ void check_strict_packed(const double (&m)[D], double
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 if (q >= k) break;
-                sm[q] = signed_min(a[q], b[q]);
+                sm[q] = signed_min_packed(a[q], b[q]);
                 t[2 * q] = a[q] + b[q];
                 t[2 * q + 1] = a[q] - b[q];
             }
-            h_packed(t, h, 2 * k, wb, T, K);
+            h_packed<CL>(t, h, 2 * k, wb, T, K);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 if (q >= k) break;

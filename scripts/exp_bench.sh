@@ -8,6 +8,6 @@ for L in ${LIBS:-""}; do
   [ ${#TS[@]} -eq 0 ] && TS=("")
   for T in "${TS[@]}"; do
     QAMR_LIB=$L QAMR_TUNE=$T timeout -k 10 300 python bench.py --steps ${STEPS:-3} --warmup 1 --cpu-seconds 0 ${BENCH_ARGS:-} > gpurun_out/exp.log 2>&1 || { tail -5 gpurun_out/exp.log; exit 1; }
-    python -c "import json;d=json.loads(open('gpurun_out/exp.log').read().strip().splitlines()[-1]);print('${L:-default}', '$T', d['value'], d['roofline']['avg_launch_us'], {k:round(v['avg_us'],1) for k,v in d['kernels'].items()})"
+    python -c "import json;d=json.loads(open('gpurun_out/exp.log').read().strip().splitlines()[-1]);print('${L:-default}', '$T', d['value'], (d.get('roofline') or {}).get('avg_launch_us'), {k:round(v['avg_us'],1) for k,v in d['kernels'].items()})"
   done
 done
