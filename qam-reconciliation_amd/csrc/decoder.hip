@@ -208,6 +208,9 @@ __device__ __forceinline__ void stage_tables(typename Arith<AR>::Tab *lds, const
 #ifndef QR_CHECK_PREFETCH
 #define QR_CHECK_PREFETCH 1
 #endif
+#ifndef QR_PACK_PREFETCH
+#define QR_PACK_PREFETCH 0
+#endif
 template <int D, int MODE, bool NT>
 struct CheckIn {
     double p[D], c[D];
@@ -345,7 +348,7 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
     // The packed strict update needs the registers the prefetched gathers would hold:
     // with them it runs at 3 waves/SIMD (142 VGPRs) or spills at 4; without, 4 waves and
     // 4.54 vs 4.96 ms per launch (MI355X, configs[2]).
-    constexpr bool kPrefetch = QR_CHECK_PREFETCH && !(AR == kStrict && QR_STRICT_PACK);
+    constexpr bool kPrefetch = QR_CHECK_PREFETCH && (QR_PACK_PREFETCH || !(AR == kStrict && QR_STRICT_PACK));
     CheckIn<D, MODE, NT> nx;
     nx.load(a, ci, f);
     for (int j = 0; j < a.g.per; ++j) {

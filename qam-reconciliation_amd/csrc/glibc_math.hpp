@@ -56,8 +56,11 @@ namespace qr {
 struct GlibcLogK {
     double invc, w, c, pad;
 };
+// ex holds the 128 exp entries twice (ex[i + 128] = ex[i]): the strict box-plus indexes it
+// by the low BYTE of ki, which gfx9 reads with an SDWA byte select inside the address shift
+// (one instruction instead of an and + shift); glibc's own index ki % 128 reads the same data.
 struct GlibcTables {
-    double2 ex[128];
+    double2 ex[256];
     double2 lg[128];
     GlibcLogK lk[128];
 };
@@ -66,8 +69,8 @@ __host__ __device__ constexpr int glibc_log_k_of_index(int i) { return i <= 80 ?
 
 inline void build_glibc_tables(GlibcTables *t) {
     for (int i = 0; i < 128; ++i) {
-        t->ex[i].x = __builtin_bit_cast(double, kGxTab[2 * i]);
-        t->ex[i].y = __builtin_bit_cast(double, kGxTab[2 * i + 1]);
+        t->ex[i].x = t->ex[i + 128].x = __builtin_bit_cast(double, kGxTab[2 * i]);
+        t->ex[i].y = t->ex[i + 128].y = __builtin_bit_cast(double, kGxTab[2 * i + 1]);
         t->lg[i].x = kGlTab[2 * i];
         t->lg[i].y = kGlTab[2 * i + 1];
         const int k = glibc_log_k_of_index(i);
@@ -308,7 +311,7 @@ __host__ __device__ __forceinline__ double g_exp_neg(double x, const GlibcTables
 #ifdef QR_EXPERIMENT_UNIFORM_EXP_IDX  // timing only (wrong results): a conflict-free broadcast read
     const double2 e = T.ex[__builtin_amdgcn_readfirstlane(ki) & 127u];
 #else
-    const double2 e = T.ex[ki & 127u];
+    const double2 e = T.ex[ki & 255u];  // = entry ki % 128 (GlibcTables: ex is stored twice)
 #endif
     const double r2 = r * r;
     const double p23 = __builtin_fma(r, kGxC3, K.c2);

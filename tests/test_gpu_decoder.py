@@ -284,3 +284,33 @@ def test_decode_device_graph_capture(gpu):
             assert torch.equal(fin.view(torch.int64), ref[0].view(torch.int64)), split
     finally:
         _lib.tune_set("split", saved)
+
+
+def test_strict_clamp_paths(gpu):
+    """The strict check sweep picks its clamp of the h arguments per batch (decoder.hip
+    QR_STRICT_FINITE): every LAPPR below 2^e (e = 1000 - (max_it + 2) log2(dv_max + 1)) ->
+    max(-|t|, -700); otherwise (inf, NaN, or finite but huge) the NaN-preserving clamp.
+    Both are bit-identical to the reference's h (decoder.pyx:41-45) on arguments far beyond
+    the 37.5 where h becomes 0, in batches that differ only in one frame."""
+    from qamr import codes
+
+    vid, cid = codes.regular_code(1008)
+    dec = _decoder(vid, cid)
+    orc = O.OracleCode(vid, cid)
+    rng = np.random.default_rng(11)
+    B = 128
+    sig = rng.uniform(0.55, 1.0, B)[:, None]
+    word = rng.integers(0, 2, (B, 1008)).astype(np.uint8)
+    synd = np.stack([orc.eval_syndrome(w) for w in word])
+    llr = 2 / sig ** 2 * ((1 - 2.0 * word) + sig * rng.standard_normal((B, 1008)))
+    llr[:40] *= rng.choice([300.0, 1e3, 1e6], (40, 1))          # box-plus arguments >> 700
+    llr[40:50, :60] *= 1e12
+    cases = {"bounded": llr.copy()}
+    x = llr.copy(); x[3, 7] = np.inf; cases["inf"] = x
+    x = llr.copy(); x[5, 9] = np.nan; cases["nan"] = x
+    x = llr.copy(); x[60, 11] = 1e300; cases["huge"] = x           # finite, above the bound
+    for name, l in cases.items():
+        s1, i1, f1 = dec.decode_batch(l, synd, 50)
+        s2, i2, f2 = orc.decode_batch(l, synd, 50)
+        assert np.array_equal(s1, s2) and np.array_equal(i1, i2), name
+        assert_bit_exact(f1, f2)
