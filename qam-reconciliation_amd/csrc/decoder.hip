@@ -669,7 +669,7 @@ static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
 // Runtime tuning knobs (qr_tune_set); defaults picked by scripts/tune.py on MI355X.
 struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3}, math{kStrict}, eps_max{40},
-        lds_pad_kb{0}, compact{1};
+        lds_pad_kb{0}, compact{1}, side{1};
 };
 static Tuning g_tune;
 
@@ -971,6 +971,27 @@ static int run_split2(const Plan &P, int max_it) {
     const int ld = P.ld, h = ld / 2;
     const int A0 = 0, A1 = h, B0 = h, B1 = ld;
     auto row = [&](int t) { return P.w.unsat + (size_t)t * ld; };
+    // Knob side (default 1): the check sweeps of the small degree classes (DVB-S2: the one
+    // degree-6 check) run on the variable stream right after the variable sweep they follow,
+    // under the other half's big check launch, instead of as a ~30 us launch of their own on
+    // the critical check stream.  Per frame the order is unchanged: var(t) -> side checks
+    // (t+1) -> [event] big checks(t+1) -> status(t) -> compaction -> [event] var(t+1).
+    int big = 0;
+    int64_t side_edges = 0;
+    for (int k = 1; k < (int)code->classes.size(); ++k)
+        if (code->classes[k].n > code->classes[big].n) big = k;
+    for (int k = 0; k < (int)code->classes.size(); ++k)
+        if (k != big) side_edges += code->classes[k].n * code->classes[k].degree;
+    const bool side = g_tune.side.load() && code->classes.size() > 1 && side_edges * 8 <= code->E;
+    auto checks_main = [&](int t, int f0, int f1) {  // check sweep t >= 2 on the check stream
+        if (!side) return launch_checks<kNormal>(C, P.post, row(t - 1), f0, f1);
+        const DegreeClass &cls = code->classes[big];
+        return P.nt ? launch_check_class<kNormal, true>(C, cls, P.post, row(t - 1), f0, f1)
+                    : launch_check_class<kNormal, false>(C, cls, P.post, row(t - 1), f0, f1);
+    };
+    auto checks_side = [&](int t, int f0, int f1) {  // the other classes of check sweep t, on V.s
+        return side ? launch_checks<kNormal>(V, P.post, row(t - 1), f0, f1, big) : (int)QR_OK;
+    };
     int rc;
     QR_HIP(hipEventRecord(fork, P.s));
     QR_HIP(hipStreamWaitEvent(V.s, fork, 0));
@@ -979,25 +1000,27 @@ static int run_split2(const Plan &P, int max_it) {
     for (int t = 1; t <= max_it; ++t) {
         QR_HIP(hipStreamWaitEvent(V.s, cA, 0));
         if ((rc = launch_var<false>(V, A0, A1))) return rc;
+        if (t < max_it && (rc = checks_side(t + 1, A0, A1))) return rc;
         QR_HIP(hipEventRecord(vA, V.s));
         if (t == 1) {
             if ((rc = launch_checks<kFirst>(C, P.post, row(0), B0, B1))) return rc;
         } else {
             QR_HIP(hipStreamWaitEvent(P.s, vB, 0));
-            if ((rc = launch_checks<kNormal>(C, P.post, row(t - 1), B0, B1))) return rc;
+            if ((rc = checks_main(t, B0, B1))) return rc;
             if ((rc = launch_status(P, B0, B1, t - 1, 0, 0, row(t - 1)))) return rc;
             if ((rc = launch_compact(P, B0, B1))) return rc;
         }
         QR_HIP(hipEventRecord(cB, P.s));
         if (t < max_it) {
             QR_HIP(hipStreamWaitEvent(P.s, vA, 0));
-            if ((rc = launch_checks<kNormal>(C, P.post, row(t), A0, A1))) return rc;
+            if ((rc = checks_main(t + 1, A0, A1))) return rc;
             if ((rc = launch_status(P, A0, A1, t, 0, 0, row(t)))) return rc;
             if ((rc = launch_compact(P, A0, A1))) return rc;
             QR_HIP(hipEventRecord(cA, P.s));
         }
         QR_HIP(hipStreamWaitEvent(V.s, cB, 0));
         if ((rc = launch_var<false>(V, B0, B1))) return rc;
+        if (t < max_it && (rc = checks_side(t + 1, B0, B1))) return rc;
         QR_HIP(hipEventRecord(vB, V.s));
     }
     // join: everything after (final parity check, status) follows both sweeps
@@ -1222,7 +1245,7 @@ int qr_tune_set(const char *name, int64_t value) {
                         : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
                         : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
                         : n == "math"     ? &g_tune.math     : n == "lds_pad_kb" ? &g_tune.lds_pad_kb : n == "eps_max"   ? &g_tune.eps_max
-                        : n == "compact" ? &g_tune.compact : n == "demap_fast" ? &g_demap_fast : nullptr;
+                        : n == "compact" ? &g_tune.compact : n == "side" ? &g_tune.side : n == "demap_fast" ? &g_demap_fast : nullptr;
     if (!k) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     if (value < 0 || value > 4096) return set_error(QR_EVALUE, "tuning value out of range");
     k->store((int)value);
@@ -1235,7 +1258,7 @@ int qr_tune_get(const char *name, int64_t *value) {
                               : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
                               : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
                               : n == "math"     ? &g_tune.math     : n == "lds_pad_kb" ? &g_tune.lds_pad_kb : n == "eps_max"   ? &g_tune.eps_max
-                              : n == "compact" ? &g_tune.compact : n == "demap_fast" ? &g_demap_fast : nullptr;
+                              : n == "compact" ? &g_tune.compact : n == "side" ? &g_tune.side : n == "demap_fast" ? &g_demap_fast : nullptr;
     if (!k || !value) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     *value = k->load();
     return QR_OK;
