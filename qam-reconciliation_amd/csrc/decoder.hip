@@ -606,15 +606,26 @@ __global__ void k_status(int f0, int f1, int t, int final_call, int32_t final_it
 
 // The still-running frames of [f0, f1) in ascending order -> list[f0 + 0 .. count).
 // One workgroup of 1024 threads: per 1024-frame chunk a wave ballot, the waves' counts
-// through LDS, one store per running frame.
-__global__ void __launch_bounds__(1024) k_compact(int f0, int f1, const uint8_t *__restrict__ active,
-                                                  int32_t *__restrict__ list, int32_t *__restrict__ count) {
+// through LDS, one store per running frame.  STATUS: the status update of sweep t
+// (k_status, never the final call) is applied first, frame by frame, by the same thread:
+// one launch instead of two between the check sweeps of the two-stream schedule.
+template <bool STATUS>
+__global__ void __launch_bounds__(1024) k_compact(int f0, int f1, uint8_t *__restrict__ active,
+                                                  int32_t *__restrict__ list, int32_t *__restrict__ count, int t,
+                                                  const uint8_t *__restrict__ unsat_t, uint8_t *__restrict__ success,
+                                                  int32_t *__restrict__ iters) {
     __shared__ int wsum[16];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int base = 0;  // running count (every thread keeps the same value)
     for (int c0 = f0; c0 < f1; c0 += 1024) {
         const int f = c0 + (int)threadIdx.x;
-        const bool a = f < f1 && active[f];
+        bool a = f < f1 && active[f];
+        if (STATUS && a && !unsat_t[f]) {  // k_status: satisfied -> (1, t), stops
+            success[f] = 1;
+            iters[f] = t;
+            active[f] = 0;
+            a = false;
+        }
         const uint64_t m = __ballot(a);
         if (lane == 0) wsum[w] = __popcll(m);
         __syncthreads();
@@ -871,7 +882,19 @@ static int launch_status(const Plan &P, int f0, int f1, int t, int final_call, i
 // Rebuild the active-frame list of [f0, f1) after a status update (no-op without compaction).
 static int launch_compact(const Plan &P, int f0, int f1) {
     if (!P.compact) return QR_OK;
-    k_compact<<<1, 1024, 0, P.s>>>(f0, f1, P.w.active, P.w.alist, const_cast<int32_t *>(P.count_of(f0)));
+    k_compact<false><<<1, 1024, 0, P.s>>>(f0, f1, P.w.active, P.w.alist, const_cast<int32_t *>(P.count_of(f0)), 0,
+                                          nullptr, nullptr, nullptr);
+    QR_LAUNCH_CHECK();
+    return QR_OK;
+}
+
+// Status update of sweep t (not the final call) + list rebuild of [f0, f1): one launch with
+// compaction, k_status alone without.
+static int launch_status_compact(const Plan &P, int f0, int f1, int t, const uint8_t *unsat_t) {
+    if (!P.compact) return launch_status(P, f0, f1, t, 0, 0, unsat_t);
+    ProfScope ps("status", P.s);
+    k_compact<true><<<1, 1024, 0, P.s>>>(f0, f1, P.w.active, P.w.alist, const_cast<int32_t *>(P.count_of(f0)), t,
+                                         unsat_t, P.success, P.iters);
     QR_LAUNCH_CHECK();
     return QR_OK;
 }
@@ -886,8 +909,7 @@ static int run_flat(const Plan &P, int max_it) {
             if ((rc = launch_checks<kFirst>(P, P.post, unsat_prev, 0, ld))) return rc;
         } else {
             if ((rc = launch_checks<kNormal>(P, P.post, unsat_prev, 0, ld))) return rc;
-            if ((rc = launch_status(P, 0, ld, t - 1, 0, 0, unsat_prev))) return rc;
-            if ((rc = launch_compact(P, 0, ld))) return rc;
+            if ((rc = launch_status_compact(P, 0, ld, t - 1, unsat_prev))) return rc;
         }
         if ((rc = launch_var<false>(P, 0, ld))) return rc;
     }
@@ -919,15 +941,13 @@ static int run_split(const Plan &P, int max_it) {
         } else {
             if ((rc = launch_checks<kNormal>(P, P.post, row(t - 1), B0, B1, big))) return rc;
             if ((rc = launch_fused<kNormal>(P, cls, row(t - 1), B0, B1, A0, A1))) return rc;
-            if ((rc = launch_status(P, B0, B1, t - 1, 0, 0, row(t - 1)))) return rc;
-            if ((rc = launch_compact(P, B0, B1))) return rc;
+            if ((rc = launch_status_compact(P, B0, B1, t - 1, row(t - 1)))) return rc;
         }
         if (t < max_it) {
             // [C_A(t+1) | V_B(t)]
             if ((rc = launch_checks<kNormal>(P, P.post, row(t), A0, A1, big))) return rc;
             if ((rc = launch_fused<kNormal>(P, cls, row(t), A0, A1, B0, B1))) return rc;
-            if ((rc = launch_status(P, A0, A1, t, 0, 0, row(t)))) return rc;
-            if ((rc = launch_compact(P, A0, A1))) return rc;
+            if ((rc = launch_status_compact(P, A0, A1, t, row(t)))) return rc;
         } else {
             if ((rc = launch_var<false>(P, B0, B1))) return rc;
         }
@@ -1007,15 +1027,13 @@ static int run_split2(const Plan &P, int max_it) {
         } else {
             QR_HIP(hipStreamWaitEvent(P.s, vB, 0));
             if ((rc = checks_main(t, B0, B1))) return rc;
-            if ((rc = launch_status(P, B0, B1, t - 1, 0, 0, row(t - 1)))) return rc;
-            if ((rc = launch_compact(P, B0, B1))) return rc;
+            if ((rc = launch_status_compact(P, B0, B1, t - 1, row(t - 1)))) return rc;
         }
         QR_HIP(hipEventRecord(cB, P.s));
         if (t < max_it) {
             QR_HIP(hipStreamWaitEvent(P.s, vA, 0));
             if ((rc = checks_main(t + 1, A0, A1))) return rc;
-            if ((rc = launch_status(P, A0, A1, t, 0, 0, row(t)))) return rc;
-            if ((rc = launch_compact(P, A0, A1))) return rc;
+            if ((rc = launch_status_compact(P, A0, A1, t, row(t)))) return rc;
             QR_HIP(hipEventRecord(cA, P.s));
         }
         QR_HIP(hipStreamWaitEvent(V.s, cB, 0));
