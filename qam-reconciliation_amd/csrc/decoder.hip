@@ -266,10 +266,19 @@ constexpr int kPackMaxDeg = 10;
 #ifndef QR_STRICT_UNCLAMPED
 #define QR_STRICT_UNCLAMPED 0
 #endif
-// LDS of the packed strict update: one kPackWaveDoubles buffer per wavefront of a block.
+// QR_PACK_PAIR: each thread updates two checks per loop step with their log arguments packed
+// together (strict_pack.hpp check_strict_packed_n<D, CL, 2>): one partly filled slice per kind
+// and round for both checks instead of one each.
+#ifndef QR_PACK_PAIR
+#define QR_PACK_PAIR 0
+#endif
+constexpr int kPackPairMaxDeg = 8;
+// LDS of the packed strict update: one buffer per wavefront of a block (64 lanes x the
+// arguments of one round, + one slice of slack).
+constexpr int kPackWaveStride = QR_PACK_PAIR ? 64 * 2 * kPackMaxJobs + 64 : kPackWaveDoubles;
 template <int AR>
 struct PackLds {
-    static constexpr int doubles = (AR == kStrict && QR_STRICT_PACK) ? 4 * kPackWaveDoubles : 1;
+    static constexpr int doubles = (AR == kStrict && QR_STRICT_PACK) ? 4 * kPackWaveStride : 1;
 };
 
 template <int AR, int D, bool NT, bool FIN = false>
@@ -280,7 +289,7 @@ __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m
     const double s = sb ? -1.0 : 1.0;
     if constexpr (AR == kStrict && QR_STRICT_PACK && D <= kPackMaxDeg) {
         double out[D];
-        double *wb = hb + (threadIdx.x >> 6) * kPackWaveDoubles;
+        double *wb = hb + (threadIdx.x >> 6) * kPackWaveStride;
         if constexpr (FIN) {
 #if QR_STRICT_UNCLAMPED
             // Every h argument of the check is |F +- m|, |B +- m| or |F +- B|, and |F|, |B| <=
@@ -349,6 +358,49 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
     // with them it runs at 3 waves/SIMD (142 VGPRs) or spills at 4; without, 4 waves and
     // 4.54 vs 4.96 ms per launch (MI355X, configs[2]).
     constexpr bool kPrefetch = QR_CHECK_PREFETCH && (QR_PACK_PREFETCH || !(AR == kStrict && QR_STRICT_PACK));
+    if constexpr (QR_PACK_PAIR && AR == kStrict && QR_STRICT_PACK && MODE != kParityOnly && D <= kPackPairMaxDeg) {
+        // two checks per step (ci, ci + nsub); a lone last check takes the single update
+        double *wb = hb + (threadIdx.x >> 6) * kPackWaveStride;
+        const uint32_t b8 = (uint32_t)f * 8u;
+        constexpr int CL = FIN ? kClampFinite : kClampFull;
+        for (int j = 0; j < a.g.per; j += 2) {
+            if (ci >= a.n_checks) break;
+            const bool two = (j + 1 < a.g.per) && ci + nsub < a.n_checks;  // wave-uniform
+            CheckIn<D, MODE, NT> x[2];
+            double m[2][D];
+            x[0].load(a, ci, f);
+            if (two) x[1].load(a, ci + nsub, f);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (c == 1 && !two) break;
+                x[c].load_c(a, f);
+                uint32_t par = x[c].sb;
+#pragma unroll
+                for (int i = 0; i < D; ++i) {
+                    const double p = x[c].p[i];
+                    if (MODE != kFirst) par ^= (p < 0.0) ? 1u : 0u;   // decoder.pyx:243-246
+                    m[c][i] = (MODE == kNormal) ? p - x[c].c[i] : p;   // :296-297
+                }
+                if (MODE != kFirst) bad |= (par == 1u) ? 1u : 0u;
+            }
+            if (two) {
+                double out[2][D];
+                check_strict_packed_n<D, CL, 2>(m, out, wb, tab, K);
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const double sg = x[c].sb ? -1.0 : 1.0;
+#pragma unroll
+                    for (int i = 0; i < D; ++i)
+                        if (live) st_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + x[c].base + i), ld), b8, ld, sg * out[c][i]);
+                }
+            } else {
+                check_exact<AR, D, NT, FIN>(a, m[0], x[0].base, x[0].sb, b8, tab, K, hb, live);
+            }
+            ci += 2 * nsub;
+        }
+        if (MODE != kFirst && bad && act && live) a.unsat[f] = 1;
+        return;
+    }
     CheckIn<D, MODE, NT> nx;
     nx.load(a, ci, f);
     for (int j = 0; j < a.g.per; ++j) {

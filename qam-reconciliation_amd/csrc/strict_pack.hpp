@@ -58,10 +58,11 @@ __host__ __device__ constexpr int pack_out_round(int D, int i) {
 // and for every t > 37.5 exp(-t) < 2^-54, so u = fl(1.0 + exp(-t)) == 1.0 and h == +0 in all
 // three modes: the same bits.
 enum { kClampNone = 0, kClampFull = 1, kClampFinite = 2 };
-template <int CL = kClampFull>
+template <int CL = kClampFull, int MJ = kPackMaxJobs>
 __device__ __forceinline__ void h_packed(const double *t, double *h, int nj, double *wb, const GlibcTables &T,
                                          const GlibcK &K) {
-    constexpr int S = kPackWaveDoubles;
+    constexpr int kPackMaxJobs = MJ;  // (shadows the namespace constant: MJ arguments per lane)
+    constexpr int S = 64 * MJ + 64;
     const uint32_t lane = __lane_id();
     uint32_t addr[kPackMaxJobs];  // byte address of the argument's slot
     uint32_t nN = 0;              // wave-uniform: near-1 arguments written so far
@@ -139,49 +140,73 @@ __device__ __forceinline__ double signed_min_packed(double a, double b) {
 // decoder.pyx:322-369 for one check of degree D (>= 2): out[i] = c2v of edge i before
 // the syndrome sign.  The same box-plus (operands and box_plus_strict's operation order)
 // as check_exact<kStrict>, evaluated round by round.
+// NC checks of degree D side by side (the same rounds; their log arguments packed together:
+// one partly filled slice per kind and round for all NC checks instead of one per check).
+template <int D, int CL = kClampFull, int NC = 1>
+__device__ __forceinline__ void check_strict_packed_n(const double (&m)[NC][D], double (&out)[NC][D], double *wb,
+                                                      const GlibcTables &T, const GlibcK &K) {
+    if constexpr (D == 2) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            out[c][0] = m[c][1];
+            out[c][1] = m[c][0];
+        }
+    } else {
+        double F[NC][D], Bv[NC][D];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            F[c][0] = m[c][0];
+            Bv[c][D - 1] = m[c][D - 1];
+        }
+#pragma unroll
+        for (int r = 1; r <= D - 2; ++r) {
+            // the round's box-plus: kind 0 = F_r, 1 = B_{D-1-r}, 2 = O_i (the same list for every check)
+            int kind[4], idx[4];
+            int k = 0;
+            kind[k] = 0, idx[k] = r, ++k;
+            kind[k] = 1, idx[k] = D - 1 - r, ++k;
+#pragma unroll
+            for (int i = 1; i <= D - 2; ++i)
+                if (pack_out_round(D, i) == r) kind[k] = 2, idx[k] = i, ++k;
+            // box_plus_strict_t: (sm + h(|a + b|)) - h(|a - b|)
+            double t[8 * NC], h[8 * NC], sm[4 * NC];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (q >= k) break;
+                    const double a = kind[q] == 0 ? F[c][r - 1] : kind[q] == 1 ? Bv[c][D - r] : F[c][idx[q] - 1];
+                    const double b = kind[q] == 0 ? m[c][r] : kind[q] == 1 ? m[c][D - 1 - r] : Bv[c][idx[q] + 1];
+                    sm[4 * c + q] = signed_min_packed(a, b);
+                    t[2 * (k * c + q)] = a + b;
+                    t[2 * (k * c + q) + 1] = a - b;
+                }
+            }
+            h_packed<CL, 8 * NC>(t, h, 2 * k * NC, wb, T, K);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (q >= k) break;
+                    const double v = (sm[4 * c + q] + h[2 * (k * c + q)]) - h[2 * (k * c + q) + 1];
+                    if (kind[q] == 0) F[c][idx[q]] = v;
+                    else if (kind[q] == 1) Bv[c][idx[q]] = v;
+                    else out[c][idx[q]] = v;
+                }
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            out[c][0] = Bv[c][1];
+            out[c][D - 1] = F[c][D - 2];
+        }
+    }
+}
 template <int D, int CL = kClampFull>
 __device__ __forceinline__ void check_strict_packed(const double (&m)[D], double (&out)[D], double *wb,
                                                     const GlibcTables &T, const GlibcK &K) {
-    if constexpr (D == 2) {
-        out[0] = m[1];
-        out[1] = m[0];
-    } else {
-        double F[D], Bv[D];
-        F[0] = m[0];
-        Bv[D - 1] = m[D - 1];
-#pragma unroll
-        for (int r = 1; r <= D - 2; ++r) {
-            // the round's box-plus: kind 0 = F_r, 1 = B_{D-1-r}, 2 = O_i
-            double a[4], b[4];
-            int kind[4], idx[4];
-            int k = 0;
-            a[k] = F[r - 1], b[k] = m[r], kind[k] = 0, idx[k] = r, ++k;
-            a[k] = Bv[D - r], b[k] = m[D - 1 - r], kind[k] = 1, idx[k] = D - 1 - r, ++k;
-#pragma unroll
-            for (int i = 1; i <= D - 2; ++i)
-                if (pack_out_round(D, i) == r) a[k] = F[i - 1], b[k] = Bv[i + 1], kind[k] = 2, idx[k] = i, ++k;
-            // box_plus_strict_t: (sm + h(|a + b|)) - h(|a - b|)
-            double t[8], h[8], sm[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (q >= k) break;
-                sm[q] = signed_min_packed(a[q], b[q]);
-                t[2 * q] = a[q] + b[q];
-                t[2 * q + 1] = a[q] - b[q];
-            }
-            h_packed<CL>(t, h, 2 * k, wb, T, K);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (q >= k) break;
-                const double v = (sm[q] + h[2 * q]) - h[2 * q + 1];
-                if (kind[q] == 0) F[idx[q]] = v;
-                else if (kind[q] == 1) Bv[idx[q]] = v;
-                else out[idx[q]] = v;
-            }
-        }
-        out[0] = Bv[1];
-        out[D - 1] = F[D - 2];
-    }
+    check_strict_packed_n<D, CL, 1>(reinterpret_cast<const double(&)[1][D]>(m), reinterpret_cast<double(&)[1][D]>(out),
+                                    wb, T, K);
 }
 
 }  // namespace qr
