@@ -54,7 +54,7 @@ struct Arith {  // kFast, kEps: MathTables (10 KiB) in LDS
     }
 };
 template <>
-struct Arith<kStrict> {  // GlibcTables (4 KiB) in LDS
+struct Arith<kStrict> {  // GlibcTables (10 KiB) in LDS
     using Tab = GlibcTables;
     using Regs = GlibcK;
     static __device__ __forceinline__ Regs regs() { return GlibcK::pinned(); }
