@@ -314,3 +314,10 @@ def test_strict_clamp_paths(gpu):
         s2, i2, f2 = orc.decode_batch(l, synd, 50)
         assert np.array_equal(s1, s2) and np.array_equal(i1, i2), name
         assert_bit_exact(f1, f2)
+    # max_it = 600: (600 + 2) log2(dv_max + 1) > 1000, the flag is cleared without a test
+    # (the decode keeps the NaN-preserving clamp whatever the inputs)
+    l = llr[:64].copy()
+    s1, i1, f1 = dec.decode_batch(l, synd[:64], 600)
+    s2, i2, f2 = orc.decode_batch(l, synd[:64], 600)
+    assert np.array_equal(s1, s2) and np.array_equal(i1, i2)
+    assert_bit_exact(f1, f2)
