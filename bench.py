@@ -112,9 +112,11 @@ def check_class_bytes(vid, cid, degree, B):
 
 
 # ----------------------------------------------------------------- rank body
-def timed_region(step, sync, steps, warmup, before=None, after=None):
+def timed_region(step, sync, steps, warmup, before=None, after=None, device=None):
     """W untimed warmup steps, then EXACTLY K steps bracketed by a barrier + device
-    sync on both sides; returns the max over ranks of the timed region [s]."""
+    sync on both sides; returns the max over ranks of the timed region [s].  The
+    max-reduce runs on ``device`` (the rank's GPU under RCCL; qamr.dist stages a
+    tensor any backend cannot reduce where it lives)."""
     import torch
 
     for _ in range(warmup):
@@ -132,7 +134,7 @@ def timed_region(step, sync, steps, warmup, before=None, after=None):
     elapsed = time.perf_counter() - t0
     if after:
         after()
-    t = torch.tensor([elapsed], dtype=torch.float64)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     dist.all_reduce_max(t)
     return float(t.item())
 
@@ -145,6 +147,7 @@ class StubWork:
         self.args, self.rank = args, rank
         self.B = args.batch
         self.V, self.C, self.E = 1008, 504, 3024
+        self.dev = None  # host tensors (qamr.dist stages them for a GPU-only backend)
 
     def step(self):
         time.sleep(0.002)
@@ -345,7 +348,7 @@ def secondary(args, rank, local):
     out = {}
     for name, wl, snr, batch, steps, what in SECONDARY:
         w = Work(wl, snr, batch, args.max_iter, args.alpha, args.seed, rank, local)
-        el = timed_region(w.step, w.sync, steps, 1)
+        el = timed_region(w.step, w.sync, steps, 1, device=w.dev)
         out[name] = {"frames_per_s": round(w.B * steps / el, 1), "ms_per_step": round(1e3 * el / steps, 3),
                      "steps": steps, "batch": w.B, "snr_db": w.snr, "mean_iterations": round(w.mean_iterations(), 3),
                      "what": what}
@@ -482,7 +485,7 @@ def main(argv=None):
             import qamr
             qamr.profile_enable(False)
 
-    elapsed = timed_region(w.step, w.sync, args.steps, args.warmup, before, after)
+    elapsed = timed_region(w.step, w.sync, args.steps, args.warmup, before, after, device=w.dev)
     counters = w.counters()
     dist.all_reduce_sum(counters)
     total_frames = world * w.B * args.steps

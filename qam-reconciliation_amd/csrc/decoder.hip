@@ -705,7 +705,7 @@ struct DecodeWs {
 };
 
 static size_t ws_bytes(const qr_code *code, int ld, int max_it) {
-    const int rows = (max_it > 0 ? max_it : 0) + 2;
+    const int64_t rows = (int64_t)(max_it > 0 ? max_it : 0) + 2;  // no int overflow at INT_MAX
     return align_up((size_t)code->E * ld * sizeof(double), 256) + align_up((size_t)ld, 256) +
            align_up((size_t)rows * ld, 256) + align_up((size_t)code->fb_rows * ld * sizeof(double), 256) +
            align_up((size_t)ld * sizeof(int32_t), 256) + 256;
@@ -714,7 +714,7 @@ static size_t ws_bytes(const qr_code *code, int ld, int max_it) {
 static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
     DecodeWs w;
     char *p = (char *)base;
-    const int rows = (max_it > 0 ? max_it : 0) + 2;
+    const int64_t rows = (int64_t)(max_it > 0 ? max_it : 0) + 2;  // no int overflow at INT_MAX
     w.c2v = (double *)p;
     p += align_up((size_t)code->E * ld * sizeof(double), 256);
     w.active = (uint8_t *)p;
@@ -1110,13 +1110,15 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
         return set_error(QR_EVALUE, "decode: workspace too small (%zu < %zu)", ws_size, ws_bytes(code, ld, max_it));
     DeviceGuard dg(code->device);
     Plan P{code, B, ld, lappr, synd, final_post, success, iters, carve(code, ld, max_it, ws_ptr), g_tune.nt.load() != 0, s};
-    const int rows = (max_it > 0 ? max_it : 0) + 2;
+    const int64_t rows = (int64_t)(max_it > 0 ? max_it : 0) + 2;  // no int overflow at INT_MAX
     int rc;
     QR_HIP(hipMemsetAsync(P.w.unsat, 0, (size_t)rows * ld, s));
     k_init_status<<<(ld + 255) / 256, 256, 0, s>>>(B, ld, P.w.active, success, iters, P.w.acount + 2);
     QR_LAUNCH_CHECK();
     // the finite flag (QR_STRICT_FINITE): bound 2^e with e = 1000 - (max_it + 2) log2(dv_max + 1)
-    const int fin_e = 1000 - (int)std::ceil((std::max(max_it, 0) + 2) * std::log2((double)code->max_dv + 1.0));
+    // (in double, clamped before the cast: max_it may be as large as INT_MAX)
+    const double fin_x = ((double)std::max(max_it, 0) + 2.0) * std::log2((double)code->max_dv + 1.0);
+    const int fin_e = fin_x > 999.0 ? 0 : 1000 - (int)std::ceil(fin_x);
     if (fin_e < 1) {
         QR_HIP(hipMemsetAsync(P.w.acount + 2, 0, sizeof(int32_t), s));
     } else if (g_tune.math.load() == kStrict) {

@@ -14,6 +14,7 @@ many independent frames per launch -- the path the benchmark measures.
 from __future__ import annotations
 
 import ctypes as C
+from collections import OrderedDict
 
 import numpy as np
 
@@ -60,7 +61,7 @@ class Decoder:
         check(L.qr_code_info(h, C.byref(v), C.byref(c), C.byref(e), C.byref(dc), C.byref(dv)))
         self._V, self._C, self._E = int(v.value), int(c.value), int(e.value)
         self.max_check_degree, self.max_var_degree = int(dc.value), int(dv.value)
-        self._ws = {}  # per-stream device workspaces of decode_device
+        self._ws = OrderedDict()  # per-stream device workspaces of decode_device (LRU, capped)
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -240,17 +241,27 @@ class Decoder:
             C.c_void_p(stream.cuda_stream)), "decode_device")
         return final_fi, success, iters
 
+    #: how many per-stream workspaces a Decoder keeps (each is E*ld*8 bytes of messages)
+    max_workspaces = 2
+
     def _workspace(self, stream, need: int):
         """Device workspace (c2v messages, flags) of the decodes issued on `stream`.
         Allocated on that stream, so torch's caching allocator orders its reuse after
-        the work queued there; one per stream, so concurrent decodes never race."""
+        the work queued there; one per stream, so concurrent decodes never race.
+        Keyed by the stream handle: torch's streams come from a per-device pool and
+        live as long as the process, so a handle always names the same stream.  At
+        most ``max_workspaces`` are kept (least recently used dropped first): a dropped
+        workspace goes back to the caching allocator, which hands its memory out again
+        only after the work already queued on its stream."""
         import torch
 
         key = int(stream.cuda_stream)
-        ws = self._ws.get(key)
+        ws = self._ws.pop(key, None)
         if ws is None or ws.numel() < need:
-            self._ws.pop(key, None)
+            ws = None  # free the smaller one before allocating
+            while len(self._ws) >= max(1, int(self.max_workspaces)):
+                self._ws.popitem(last=False)
             with torch.cuda.stream(stream):
                 ws = torch.empty(need, dtype=torch.uint8, device=torch.device("cuda", self._device))
-            self._ws[key] = ws
+        self._ws[key] = ws
         return ws

@@ -28,9 +28,11 @@ def init(backend: str | None = None, device: int | None = None):
     ``backend``: "nccl" (= RCCL on ROCm; one GPU per rank), "gloo" (CPU tensors;
     the CPU tests and the several-ranks-on-one-GPU rehearsal) or None (RCCL when a
     GPU is visible).  ``device``: the GPU this rank binds (default: LOCAL_RANK).
-    The world size returned is the one the process group reports."""
+    The world size returned is the one the process group reports.
+    ``QAMR_DIST_FORCE_PG=1`` creates the process group at world size 1 too, so a
+    single-GPU run pushes every collective through RCCL (tests/test_gpu_dist.py)."""
     world, rank, local = env_world()
-    if world > 1:
+    if world > 1 or os.environ.get("QAMR_DIST_FORCE_PG") == "1":
         import torch
         import torch.distributed as dist
 
@@ -57,18 +59,56 @@ def backend():
     return None
 
 
-def _all_reduce(t, op):
-    """All-reduce in place; under gloo a GPU tensor is staged through the host."""
+def _capability(backend_name: str):
+    """Device types the backend's collectives accept.  A multi-device backend string
+    ("cpu:gloo,cuda:nccl") accepts the union of its parts."""
     import torch.distributed as dist
 
-    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+    caps = set()
+    for part in str(backend_name).split(","):
+        name = part.split(":")[-1].strip().lower()
+        caps.update(dist.Backend.backend_capability.get(name, []))
+    return caps
+
+
+def staging_device_type(backend_name: str, device_type: str):
+    """Device type a tensor living on ``device_type`` must be staged to before a
+    collective of ``backend_name``, or None when it can be reduced where it lives.
+    RCCL ("nccl") reduces GPU tensors only: a host tensor goes through the rank's GPU.
+    gloo is always given host tensors (its GPU path is not built for ROCm)."""
+    name = str(backend_name).lower()
+    if name == "gloo":
+        return None if device_type == "cpu" else "cpu"
+    caps = _capability(name)
+    if device_type in caps:
+        return None
+    return "cuda" if "cuda" in caps else "cpu"
+
+
+def _stage(t, device_type: str):
+    """Copy ``t`` to ``device_type`` (the rank's current GPU for "cuda")."""
+    import torch
+
+    if device_type == "cuda":
+        return t.to(torch.device("cuda", torch.cuda.current_device()))
+    return t.to(device_type)
+
+
+def _all_reduce(t, op):
+    """All-reduce in place.  The tensor is staged to a device the backend reduces on
+    (RCCL: the rank's GPU; gloo: the host) and copied back, so callers may hand in
+    host or GPU tensors under either backend."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
         return t
-    if dist.get_backend() == "gloo" and t.is_cuda:
-        h = t.cpu()
-        dist.all_reduce(h, op=op)
-        t.copy_(h)
-    else:
+    to = staging_device_type(dist.get_backend(), t.device.type)
+    if to is None:
         dist.all_reduce(t, op=op)
+    else:
+        s = _stage(t, to)
+        dist.all_reduce(s, op=op)
+        t.copy_(s)
     return t
 
 
@@ -100,7 +140,7 @@ def all_reduce_max(t):
 def barrier():
     import torch.distributed as dist
 
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():
         dist.barrier()
 
 

@@ -133,3 +133,78 @@ def test_bench_world_size_must_match_gpus():
     env = dict(os.environ, QAMR_BENCH_STUB="1", WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, BENCH, "--gpus", "1"], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "must agree" in r.stderr
+
+
+# ------------------------------------------------------- RCCL device capability
+def _qamr_dist():
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "qam-reconciliation_amd"))
+    from qamr import dist
+    return dist
+
+
+def test_staging_follows_backend_capability():
+    """RCCL reduces GPU tensors only (torch's Backend.backend_capability['nccl']);
+    qamr.dist stages a host tensor through the rank's GPU, and gloo gets host tensors."""
+    d = _qamr_dist()
+    assert d.staging_device_type("nccl", "cpu") == "cuda"
+    assert d.staging_device_type("nccl", "cuda") is None
+    assert d.staging_device_type("gloo", "cpu") is None
+    assert d.staging_device_type("gloo", "cuda") == "cpu"
+    assert d.staging_device_type("cpu:gloo,cuda:nccl", "cpu") is None
+    assert d.staging_device_type("cpu:gloo,cuda:nccl", "cuda") is None
+
+
+def test_bench_rank_body_under_rccl_capability(monkeypatch, capsys):
+    """The bench's whole rank body (stub GPU work) with torch.distributed faked as a
+    2-rank "nccl" group whose all_reduce rejects, as RCCL does, any tensor whose device
+    the backend cannot reduce on.  A host tensor is accepted only after qamr.dist has
+    staged it to the GPU (recorded by the stand-in for the host->GPU copy, since this
+    box has no GPU).  Round 2's timed region handed RCCL a host tensor: that fails here."""
+    import json
+    import sys
+
+    import torch
+    import torch.distributed as tdist
+
+    d = _qamr_dist()
+    sys.path.insert(0, os.path.dirname(BENCH))
+    import bench
+
+    cap = set(tdist.Backend.backend_capability["nccl"])
+    staged, seen = set(), []
+
+    def fake_stage(t, device_type):
+        assert device_type == "cuda"
+        s = t.clone()
+        staged.add(id(s))
+        return s
+
+    def fake_all_reduce(t, op=None, **kw):
+        ok = t.device.type in cap or id(t) in staged
+        seen.append((t.device.type, ok))
+        if not ok:
+            raise ValueError(f"No backend type associated with device type {t.device.type}")
+        if op == tdist.ReduceOp.SUM:
+            t.mul_(2)  # a second rank contributing the same values
+
+    monkeypatch.setattr(d, "_stage", fake_stage)
+    monkeypatch.setattr(tdist, "is_initialized", lambda: True)
+    monkeypatch.setattr(tdist, "init_process_group", lambda *a, **k: None)
+    monkeypatch.setattr(tdist, "destroy_process_group", lambda *a, **k: None)
+    monkeypatch.setattr(tdist, "get_world_size", lambda *a, **k: 2)
+    monkeypatch.setattr(tdist, "get_rank", lambda *a, **k: 0)
+    monkeypatch.setattr(tdist, "get_backend", lambda *a, **k: "nccl")
+    monkeypatch.setattr(tdist, "barrier", lambda *a, **k: None)
+    monkeypatch.setattr(tdist, "all_reduce", fake_all_reduce)
+    monkeypatch.setattr(torch.cuda, "set_device", lambda *a, **k: None)
+    for k, v in dict(QAMR_BENCH_STUB="1", QAMR_BENCH_BACKEND="nccl", WORLD_SIZE="2", RANK="0",
+                     LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29500").items():
+        monkeypatch.setenv(k, v)
+    assert bench.main(["--gpus", "2", "--steps", "2", "--warmup", "1"]) == 0
+    out = json.loads([l for l in capsys.readouterr().out.splitlines() if l.startswith("{")][-1])
+    assert out["n_gpus"] == 2 and out["config"]["backend"] == "nccl"
+    assert len(seen) >= 2 and all(ok for _, ok in seen)  # timed-region max + counter sum
+    B = out["config"]["batch_per_gpu"]
+    assert out["counters"] == [2 * 10, 2 * 1, 2 * (B - 1), 2 * 7 * (B - 1), 2 * B]

@@ -1,0 +1,121 @@
+"""The exact schedule bench.py times, checked against the oracle and the reference.
+
+bench.py decodes B = 4096 frames (ld = 4096) with the default tuning: the two-stream
+split schedule (``split = 3``: check sweeps of one frame half on the caller's stream
+beside the variable sweeps of the other half on a second stream) and active-frame
+compaction (``compact = 1``).  The N=64800 bit-exact tests elsewhere run B = 24
+(ld = 64), which takes ``run_flat``; here the batches are large enough (ld >= 512) that
+``decode_batch_device`` takes ``run_split2`` with compaction, as in the timed region.
+
+* ``test_timed_schedule_vs_oracle``: configs[2] (4-PAM 3.0 dB, B = 4096 = the bench's
+  own batch), 4-PAM 3.6 dB (both outcomes occur, so compaction reshuffles lanes), and
+  configs[3] (16-PAM 13.0 dB, demap fused, B = 4096): 16 frames spread over both halves
+  decoded by the oracle from the GPU's LAPPRs -- success, iterations and final LAPPRs
+  bit-exact; for 16-PAM the GPU-demapped LAPPRs of those frames too
+  (reference: decoder.pyx:424-433, noisemapper.pyx:544-559).
+* ``test_reference_frames_in_timed_batch``: the frames the reference itself demapped
+  and decoded (tests/golden/dvbs2.npz, dvbs2_16pam.npz) planted into such batches at a
+  column of each half: demapped LAPPRs, success, iterations and final LAPPRs identical
+  to the reference's (sims/reconciliation.pyx:143-147).
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_bit_exact, golden
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+# the tuning bench.py runs with (csrc/decoder.hip Tuning defaults)
+TIMED = dict(split=3, compact=1)
+
+
+def _assert_timed_defaults():
+    from qamr import _lib
+    for k, v in TIMED.items():
+        assert int(_lib.tune_get(k)) == v, f"bench default {k}={v} changed: update this test"
+
+
+def _pipeline(bps, snr, B, seed):
+    import torch
+    import qamr
+    from qamr import codes
+    from qamr.pipeline import SofteningPipeline
+
+    vid, cid = codes.dvbs2_like_half()
+    dec = qamr.Decoder(vid, cid)
+    pipe = SofteningPipeline(dec, bps=bps, snr_db=snr, batch=B, max_iterations=50)
+    assert pipe.ld == B and B % 512 == 0  # run_split2 territory
+    b = pipe.generate(torch.Generator(device="cuda").manual_seed(seed))
+    return vid, cid, dec, pipe, b
+
+
+def _cols(B, n=16):
+    """n frame columns spread over both halves of the split schedule."""
+    return np.unique(np.r_[np.linspace(0, B // 2 - 1, n // 2).astype(int),
+                           np.linspace(B // 2, B - 1, n // 2).astype(int)])
+
+
+@pytest.mark.parametrize("bps,snr,B", [(2, 3.0, 4096), (2, 3.6, 512), (4, 13.0, 4096)])
+def test_timed_schedule_vs_oracle(gpu, bps, snr, B):
+    import torch
+
+    _assert_timed_defaults()
+    vid, cid, dec, pipe, b = _pipeline(bps, snr, B, seed=100 + int(10 * snr))
+    lappr = pipe.demap(b)
+    fin, succ, its = pipe.decode(lappr, b)
+    torch.cuda.synchronize()
+    cols = _cols(B)
+    ct = torch.as_tensor(cols, device=lappr.device)
+    L = lappr[:, ct].T.contiguous().cpu().numpy()
+    Sy = b.synd[:, ct].T.contiguous().cpu().numpy()
+    if bps == 4:
+        onm = O.OracleNoiseMapper(bps, 2.0, pipe.noise_var, np.array([0, 1] * 8, np.uint8))
+        nh = b.nhat[:, ct].T.contiguous().cpu().numpy()
+        xs = b.x[:, ct].T.contiguous().cpu().numpy()
+        ref_l = np.stack([onm.demap_lappr_array(nh[i], xs[i]) for i in range(len(cols))])
+        assert_bit_exact(L, ref_l)
+    s2, i2, f2 = O.OracleCode(vid, cid).decode_batch(L, Sy, 50)
+    assert np.array_equal(succ[ct].cpu().numpy(), s2)
+    assert np.array_equal(its[ct].cpu().numpy(), i2)
+    assert_bit_exact(fin[:, ct].T.contiguous().cpu().numpy(), f2)
+    if snr == 3.6:
+        s_all = succ.cpu().numpy()
+        assert 0 < s_all.sum() < B  # frames stop at different iterations: compaction is exercised
+
+
+@pytest.mark.parametrize("fname,key,bps,snr,B", [("dvbs2.npz", "snr30", 2, 3.0, 4096),
+                                                 ("dvbs2.npz", "snr40", 2, 4.0, 512),
+                                                 ("dvbs2_16pam.npz", "snr130", 4, 13.0, 4096),
+                                                 ("dvbs2_16pam.npz", "snr145", 4, 14.5, 512)])
+def test_reference_frames_in_timed_batch(gpu, fname, key, bps, snr, B):
+    import torch
+    from qamr import codes
+
+    _assert_timed_defaults()
+    g = golden(fname)
+    vid, cid, dec, pipe, b = _pipeline(bps, snr, B, seed=7)
+    assert codes.code_digest(vid, cid) == str(g["digest"])
+    assert pipe.noise_var == float(g[f"{key}_noise_var"])
+    dev = b.x.device
+    x = torch.as_tensor(g[f"{key}_x"].astype(np.int64), device=dev)
+    nh = torch.as_tensor(g[f"{key}_nhat"], device=dev)
+    sy = torch.as_tensor(np.unpackbits(g[f"{key}_synd_packed"])[:dec.cnum], device=dev)
+    plant = [B // 2 - 37, B - 5]  # one column in each half
+    for c in plant:
+        b.x[:, c] = x
+        b.nhat[:, c] = nh
+        b.synd[:, c] = sy
+    lappr = pipe.demap(b)
+    fin, succ, its = pipe.decode(lappr, b)
+    torch.cuda.synchronize()
+    for c in plant:
+        assert_bit_exact(lappr[:, c].cpu().numpy(), g[f"{key}_lappr"])
+        assert (int(succ[c]), int(its[c])) == (int(g[f"{key}_success"]), int(g[f"{key}_iters"]))
+        f = fin[:, c].cpu().numpy()
+        assert np.array_equal(np.packbits(f < 0), g[f"{key}_hard_packed"])
+        if f"{key}_final" in g:
+            assert_bit_exact(f, g[f"{key}_final"])
+        else:
+            assert_bit_exact(f[g[f"{key}_sample_idx"]], g[f"{key}_sample_final"])
