@@ -87,6 +87,9 @@ def parse(argv=None):
     p.add_argument("--math", default="strict", choices=list(MATH), help="decoder arithmetic (strict = bit-exact)")
     p.add_argument("--no-alt", action="store_true", help="skip the alt_math throughput of the other arithmetics")
     p.add_argument("--no-secondary", action="store_true", help="skip the secondary configs")
+    p.add_argument("--graph", type=int, default=0, choices=[0, 1],
+                   help="1: replay each step as a captured HIP graph (kernel timings then come from the "
+                        "graph's event nodes, i.e. the last replay of the timed region)")
     return p.parse_args(argv)
 
 
@@ -198,10 +201,28 @@ class Work:
         self.V, self.C, self.E = self.dec.vnum, self.dec.cnum, self.dec.ednum
         torch.cuda.synchronize(self.dev)
 
-    def step(self):
+    def step_eager(self):
         if self.fused:
             self.pipe.demap(self.batch, out=self.lappr)
         self.pipe.decode(self.lappr, self.batch, self.final, self.succ, self.its)
+
+    def capture(self):
+        """Capture one step (demap + the whole decode schedule, both streams) as a HIP
+        graph; step() then replays it (no per-launch host overhead)."""
+        import torch
+
+        self.step_eager()  # allocates the decode workspace outside the capture
+        torch.cuda.synchronize(self.dev)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.step_eager()
+        torch.cuda.synchronize(self.dev)
+
+    def step(self):
+        if getattr(self, "graph", None) is not None:
+            self.graph.replay()
+        else:
+            self.step_eager()
 
     def sync(self):
         import torch
@@ -219,7 +240,7 @@ class Work:
     def free(self):
         import torch
 
-        for k in ("batch", "lappr", "final", "succ", "its", "pipe", "dec"):
+        for k in ("graph", "batch", "lappr", "final", "succ", "its", "pipe", "dec"):
             setattr(self, k, None)
         torch.cuda.empty_cache()
 
@@ -253,6 +274,33 @@ def copy_bandwidth(dev, nbytes=2 << 30, reps=5):
     del a, b
     torch.cuda.empty_cache()
     return gbps
+
+
+def probe_clock(w, n=8, ms=2.0):
+    """Shader clock under the decode's load, unprofiled: one eager step is enqueued, then
+    n one-wave clock probes (qr_clock_probe: shader cycles / 100 MHz realtime ticks over
+    ~ms each) on a side stream, which the GPU schedules beside the step's kernels.
+    Returns the median in GHz (None on failure)."""
+    import ctypes
+
+    import torch
+    from qamr import _lib
+
+    try:
+        L = _lib.load()
+        out = torch.zeros(2 * n, dtype=torch.int64, device=w.dev)
+        side = torch.cuda.Stream(w.dev)
+        torch.cuda.synchronize(w.dev)
+        w.step_eager()
+        time.sleep(0.05)  # let the step's first sweeps occupy the chip
+        _lib.check(L.qr_clock_probe(ctypes.c_void_p(out.data_ptr()), n, int(ms * 1e5),
+                                    ctypes.c_void_p(side.cuda_stream)))
+        torch.cuda.synchronize(w.dev)
+        o = out.cpu().numpy().reshape(n, 2)
+        ghz = sorted(float(c) / float(r) * 0.1 for c, r in o if r > 0)
+        return ghz[len(ghz) // 2] if ghz else None
+    except Exception:
+        return None
 
 
 def kernel_stats():
@@ -315,19 +363,25 @@ def roofline(args, w, kstats, dev):
                     n_all, n64 = t["valu_insts_per_launch"], t.get("valu_f64_insts_per_launch", 0)
                     # every wave64 VALU instruction (fp64 or 32-bit) holds its SIMD for one
                     # quad-cycle in this kernel (SQ_ACTIVE_INST_VALU == SQ_INSTS_VALU)
-                    clk = t.get("clock_ghz_pmc") or CLOCK_HZ / 1e9
+                    clk_pmc = t.get("clock_ghz_pmc")
+                    clk_live = probe_clock(w)
+                    clk = clk_live or clk_pmc or CLOCK_HZ / 1e9
                     busy = 4 * n_all / SIMDS / (clk * 1e9)  # s of SIMD issue time
                     valu = {"wave_insts_per_launch": int(n_all), "f64_wave_insts_per_launch": int(n64),
                             "clock_ghz": round(clk, 3),
+                            "clock_source": "live (qr_clock_probe beside an unprofiled step)" if clk_live
+                            else "profiled PMC pass" if clk_pmc else "spec",
+                            "clock_ghz_pmc": round(clk_pmc, 3) if clk_pmc else None,
                             "issue_ms": round(busy * 1e3, 3),
                             "frac": round(busy / avg_s, 4),
                             "busy_pmc": round(t["valu_busy_pmc"], 4) if t.get("valu_busy_pmc") else None,
                             "source": t.get("source"),
                             "note": "SIMD issue time of the launch's VALU instructions (4 cycles per wave64 "
-                                    "instruction) at the shader clock measured during the profiled launch "
-                                    "(GRBM_GUI_ACTIVE per XCD / launch time) over the live launch time; "
-                                    "busy_pmc = rocprofv3 VALUBusy of the profiled launch; counts from "
-                                    "profiles/pmc_traffic.json (rocprofv3 --pmc)"}
+                                    "instruction, counts from profiles/pmc_traffic.json, rocprofv3 --pmc) at the "
+                                    "shader clock read by in-kernel s_memtime/s_memrealtime probes running "
+                                    "beside an unprofiled step, over the live launch time; clock_ghz_pmc = "
+                                    "GRBM_GUI_ACTIVE per XCD / launch time of the profiled pass; busy_pmc = "
+                                    "rocprofv3 VALUBusy of the profiled launch"}
         except Exception:
             traffic = None
     copy_gbps = copy_bandwidth(dev)
@@ -427,16 +481,16 @@ def alt_math(args, w):
         if name == args.math:
             continue
         qamr._lib.tune_set("math", code)
-        w.step()
+        w.step_eager()  # (a captured graph would replay the measured arithmetic's kernels)
         w.sync()
         n_alt = 2
         ta = time.perf_counter()
         for _ in range(n_alt):
-            w.step()
+            w.step_eager()
         w.sync()
         alt[name] = round(w.B * n_alt / (time.perf_counter() - ta), 1)
     qamr._lib.tune_set("math", MATH[args.math])
-    w.step()  # leave `final` as the measured arithmetic produced it
+    w.step_eager()  # leave `final` as the measured arithmetic produced it
     w.sync()
     return alt
 
@@ -473,15 +527,24 @@ def main(argv=None):
         w = Work(args.workload, args.snr, args.batch, args.max_iter, args.alpha, args.seed, rank, local)
 
     prof = not stub and not args.no_roofline
+    graph = bool(args.graph) and not stub
+    if graph:
+        import qamr
+        if prof:  # the captured launches carry their event pairs as graph nodes
+            qamr.profile_reset()
+            qamr.profile_enable(True)
+        w.capture()
+        if prof:
+            qamr.profile_enable(False)
 
     def before():
-        if prof:
+        if prof and not graph:
             import qamr
             qamr.profile_reset()
             qamr.profile_enable(True)
 
     def after():
-        if prof:
+        if prof and not graph:
             import qamr
             qamr.profile_enable(False)
 
@@ -517,6 +580,7 @@ def main(argv=None):
         out["config"] = {"workload": args.workload, "code": w.code_name, "V": w.V, "C": w.C, "E": w.E,
                          "batch_per_gpu": w.B, "global_batch": world * w.B, "max_iterations": args.max_iter,
                          "snr_db": w.snr, "bps": w.bps, "fused_demap": w.fused, "parallelism": f"dp{world}",
+                         "hip_graph": graph,
                          "backend": dist.backend() or "none",
                          "arithmetic": args.math + (" (glibc exp/log restated: outputs bit-identical to the "
                                                     "reference)" if args.math == "strict" else

@@ -199,6 +199,13 @@ QR_API int qr_to_frame_innermost_i64(int32_t B, int32_t ld, int64_t n, const int
  * 16-B aligned pointers.  Not a reference interface. */
 QR_API int qr_stream_copy(const void *d_src, void *d_dst, int64_t bytes, void *stream);
 
+/* Shader-clock probe: n one-wave workgroups, each spinning (scalar only, s_sleep) for
+ * `realtime_ticks` of the 100 MHz constant clock and writing {shader cycles, realtime
+ * ticks} to d_out[2i], d_out[2i+1].  Launched on a side stream while the decode runs, it
+ * reads the clock the chip holds under that load without a profiler attached
+ * (MI355X_MICROARCH.md "DVFS give-back" item 6).  Not a reference interface. */
+QR_API int qr_clock_probe(int64_t *d_out, int32_t n, int64_t realtime_ticks, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1317,7 +1317,7 @@ int qr_tune_set(const char *name, int64_t value) {
                         : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
                         : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
                         : n == "math"     ? &g_tune.math     : n == "lds_pad_kb" ? &g_tune.lds_pad_kb : n == "eps_max"   ? &g_tune.eps_max
-                        : n == "compact" ? &g_tune.compact : n == "side" ? &g_tune.side : n == "demap_fast" ? &g_demap_fast : nullptr;
+                        : n == "compact" ? &g_tune.compact : n == "side" ? &g_tune.side : n == "demap_fast" ? &g_demap_fast : n == "demap_hyp" ? &g_demap_hyp : nullptr;
     if (!k) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     if (value < 0 || value > 4096) return set_error(QR_EVALUE, "tuning value out of range");
     k->store((int)value);
@@ -1330,7 +1330,7 @@ int qr_tune_get(const char *name, int64_t *value) {
                               : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
                               : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
                               : n == "math"     ? &g_tune.math     : n == "lds_pad_kb" ? &g_tune.lds_pad_kb : n == "eps_max"   ? &g_tune.eps_max
-                              : n == "compact" ? &g_tune.compact : n == "side" ? &g_tune.side : n == "demap_fast" ? &g_demap_fast : nullptr;
+                              : n == "compact" ? &g_tune.compact : n == "side" ? &g_tune.side : n == "demap_fast" ? &g_demap_fast : n == "demap_hyp" ? &g_demap_hyp : nullptr;
     if (!k || !value) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     *value = k->load();
     return QR_OK;

@@ -21,6 +21,8 @@ namespace qr {
 
 // 1 = Newton-located root + replayed bisection (bit-identical, ~5x fewer erf), 0 = brute force.
 std::atomic<int> g_demap_fast{1};
+// 1 = hypothesis-parallel kernel (k_demap_hyp) on 64-frame tiles, 0 = one lane per symbol (k_demap).
+std::atomic<int> g_demap_hyp{1};
 
 #ifndef QR_DEMAP_WAVES
 // Single-loop LLR sum: 5 waves/SIMD (96 VGPRs, 52-84 B spilled) 53.4 / 58.5 ms vs 4 waves 55.9 / 62.5 ms
@@ -52,6 +54,160 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QR_DEM
     }
 #pragma unroll
     for (int k = 0; k < BPS; ++k) lappr[(s * BPS + k) * ld + f] = out[k];
+}
+
+// ---------------------------------------------------------------------------
+// Hypothesis-parallel demapper (default for 2..64-PAM on 64-frame tiles).
+//
+// One workgroup = one symbol position s x 64 frames, W = min(M, 4) wavefronts; wave w
+// takes the hypotheses i = w, w + W, ... (the reference's loop over i,
+// noisemapper.pyx:490-530), lane = frame.  Per (frame, i) a lane runs the root search
+// for y_i (g_inv_search, :310-345, fast path), the M-term sum S_i in the reference's order
+// (:503-515) and parks q_i = dF[i] / S_i in LDS; after a barrier, wave k % W combines
+// bit k of every frame: N[k] / D[k] accumulated over i ascending (:521-530, per k exactly
+// the reference's sequence of additions), log(N) - log(D) (:534-538), times alpha.
+// The root search's certified closed form needs at most one exact F_Y per (frame, i),
+// for ~2 % of the lanes; instead of the wave running a divergent M-erf F_Y whenever any
+// of its lanes needs one, the lanes' evaluation points are compacted into LDS (ballot +
+// mbcnt) and the wave evaluates their M erf terms with one lane per (point, m), 64 / M
+// points per pass, after which each owner sums its M terms in m order (noisemapper.pyx:
+// 278-286: the same products, the same sequence of additions).  Per lane the state is
+// one search and one sum (no M-long accumulators): no scratch spill.
+// The grid strides over the (s, tile) items, so the 4 KiB of glibc tables are staged once
+// per resident workgroup.
+constexpr int kDemapHypWaves = 4;
+constexpr int kDemapHypMaxBps = 6;
+
+// rank of this lane among the set lanes of mk below it
+__device__ __forceinline__ int lane_rank(uint64_t mk) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+}
+
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// g_inv_search_fast (qamr_math.hpp) with the closed form's exact F_Y evaluated by the
+// whole wave (see above).  Every lane of the wave must call it (wave-uniform i).
+// ey / et: this wave's 64-double LDS buffers (evaluation points, erf terms).
+template <int M>
+__device__ __forceinline__ double g_inv_search_wave(const DemapTables &t, const MathTables &mt, double n_hat, int i,
+                                                    double *ey, double *et, int lane) {
+    SearchCmp cmp{&t, search_target(t, n_hat, i), 0.0, 0.0, false};
+    cmp.have = newton_root(t, mt, cmp.T, i, cmp.ystar, cmp.W);   // T lies in region i
+    double L = 0.0, H = 0.0;
+    int need = 0;
+    const bool closed = cmp.have && search_closed_prepare(cmp, L, H, need);
+    const bool ask = need != 0;
+    const uint64_t mk = __ballot(ask);
+    bool gt = false;
+    if (mk) {  // wave-uniform
+        const int cnt = __popcll(mk);
+        const int rank = lane_rank(mk);
+        if (ask) ey[rank] = (need == 1) ? L : H;
+        wave_lds_fence();
+        constexpr int P = 64 / M;  // points per pass
+        const int sub = lane / M, m = lane % M;
+        for (int base = 0; base < cnt; base += P) {   // wave-uniform trip count
+            const int item = base + sub;
+            if (item < cnt) et[lane] = (0.5 * (1 + cephes_erf((ey[item] - t.a[m]) / t.den))) * t.p[m];
+            wave_lds_fence();
+            if (ask && rank >= base && rank < base + P) {
+                const double *tt = et + (rank - base) * M;
+                double F = tt[0];                     // noisemapper.pyx:282-285, m = 0 first
+#pragma unroll
+                for (int mm = 1; mm < M; ++mm) F += tt[mm];
+                gt = F > cmp.T;                       // SearchCmp::exact(y) > 0
+            }
+            wave_lds_fence();
+        }
+    }
+    if (closed) return search_closed_finish(L, H, need, gt);
+    return search_replay(cmp);   // no certified window / outside the closed form (rare): per lane
+}
+
+template <int BPS>
+__global__ void __launch_bounds__(64 * kDemapHypWaves) k_demap_hyp(const DemapTables *__restrict__ tab,
+                                                                  const MathTables *__restrict__ gmt, int B, int ld,
+                                                                  int64_t S, const double *__restrict__ n,
+                                                                  const int64_t *__restrict__ j, double alpha,
+                                                                  double *__restrict__ lappr) {
+    constexpr int M = 1 << BPS;
+    constexpr int W = M < kDemapHypWaves ? M : kDemapHypWaves;
+    constexpr int HPW = M / W;
+    __shared__ GlibcExpLog gt;
+    __shared__ double q[M][64];
+    __shared__ double ey[W][64], et[W][64];
+    stage_glibc_exp_log(&gt, &kGlibcConst);
+    const DemapTables &t = *tab;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t tiles = ld / 64;
+    const int64_t items = S * tiles;
+    for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {   // uniform per workgroup
+        const int64_t s = it / tiles;
+        const int f = (int)(it - s * tiles) * 64 + lane;
+        const bool valid = f < B;
+        const double nv = valid ? n[s * ld + f] : 0.5;   // padding lanes: a harmless target
+        const int64_t jv = valid ? j[s * ld + f] : 0;
+        const bool jok = jv >= 0 && jv < M;
+        const int jj = jok ? (int)jv : 0;
+        const double aj = t.a[jj];
+#pragma unroll 1
+        for (int h = 0; h < HPW; ++h) {
+            const int i = w + h * W;
+            const double y = g_inv_search_wave<M>(t, *gmt, nv, i, ey[w], et[w], lane);
+            // noisemapper.pyx:503-515 in the reference's summation order (k < j, p[j], k > j)
+            // as one loop with the argument selected per lane (see demap_symbol)
+            double sum = 0;
+#pragma unroll 4
+            for (int k = 0; k < M; ++k) {
+                const double e = (2 * y - t.a[k] - aj) * (t.a[k] - aj);
+                const double arg = k < jj ? e : div_two_s2(t, e);
+                const double term = k == jj ? t.p[jj] : g_exp_full(arg, gt) * t.p[k];
+                sum += term;
+            }
+            q[i][lane] = t.dF[i] / sum;
+        }
+        __syncthreads();
+        for (int k = w; k < BPS; k += W) {
+            double N = 0, D = 0;
+#pragma unroll
+            for (int i = 0; i < M; ++i) {   // noisemapper.pyx:521-530: Gray bit k of i
+                const int mi = i >> k;
+                if ((mi * (mi + 1)) & 3) D += q[i][lane];
+                else                     N += q[i][lane];
+            }
+            const double out = (g_log_full(N, gt) - g_log_full(D, gt)) * alpha;   // :534-538, x alpha
+            if (valid) lappr[(s * BPS + k) * ld + f] = jok ? out : __builtin_nan("");
+        }
+        __syncthreads();   // q is rewritten by the next item
+    }
+}
+
+// workgroups of the grid-stride demap: enough to fill every CU several times over
+static unsigned demap_hyp_grid(int device, int64_t items) {
+    static std::atomic<int> cus[64];
+    int cu = (device >= 0 && device < 64) ? cus[device].load() : 0;
+    if (cu <= 0) {
+        if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cu <= 0)
+            cu = 256;
+        if (device >= 0 && device < 64) cus[device].store(cu);
+    }
+    const int64_t want = (int64_t)cu * 16;
+    return (unsigned)(items < want ? items : want);
+}
+
+static bool launch_demap_hyp(int bps, unsigned grid, hipStream_t st, const qr_demap *dm, int B, int ld, int64_t S,
+                             const double *n, const int64_t *j, double alpha, double *lappr) {
+    switch (bps) {
+#define QR_DEMAP_HYP(b) \
+        case b: k_demap_hyp<b><<<grid, 64 * (((1 << b) < kDemapHypWaves) ? (1 << b) : kDemapHypWaves), 0, st>>>( \
+            dm->d_tables, dm->d_mtab, B, ld, S, n, j, alpha, lappr); return true;
+        QR_DEMAP_HYP(1) QR_DEMAP_HYP(2) QR_DEMAP_HYP(3) QR_DEMAP_HYP(4) QR_DEMAP_HYP(5) QR_DEMAP_HYP(6)
+#undef QR_DEMAP_HYP
+        default: return false;
+    }
 }
 
 template <int BPS>
@@ -244,9 +400,14 @@ int demap_batch_device(const qr_demap *dm, int B, int ld, int64_t S, const doubl
     if (rc) return rc;
     DeviceGuard g(dm->device);
     ProfScope ps("demap", s);
-    const int64_t items = S * ld;
-    launch_demap_bps(dm->h.bps, g_demap_fast.load() != 0, (unsigned)((items + 255) / 256), s, dm, B, ld, S, n, j,
-                     alpha, lappr);
+    const bool fast = g_demap_fast.load() != 0;
+    if (fast && g_demap_hyp.load() != 0 && ld % kWave == 0 && dm->h.bps <= kDemapHypMaxBps) {
+        const int64_t items = S * (ld / kWave);
+        launch_demap_hyp(dm->h.bps, demap_hyp_grid(dm->device, items), s, dm, B, ld, S, n, j, alpha, lappr);
+    } else {
+        const int64_t items = S * ld;
+        launch_demap_bps(dm->h.bps, fast, (unsigned)((items + 255) / 256), s, dm, B, ld, S, n, j, alpha, lappr);
+    }
     QR_LAUNCH_CHECK();
     return QR_OK;
 }

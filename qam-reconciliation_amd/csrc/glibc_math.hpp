@@ -65,6 +65,13 @@ struct GlibcTables {
     GlibcLogK lk[128];
 };
 
+// The demapper's subset (glibc_math g_exp_full / g_log_full read only ex[ki % 128] and lg):
+// 4 KiB of LDS per workgroup instead of 10.
+struct GlibcExpLog {
+    double2 ex[128];
+    double2 lg[128];
+};
+
 __host__ __device__ constexpr int glibc_log_k_of_index(int i) { return i <= 80 ? 1 : 0; }
 
 inline void build_glibc_tables(GlibcTables *t) {
@@ -80,6 +87,15 @@ inline void build_glibc_tables(GlibcTables *t) {
         e.c = k ? kGlLn2lo : 0.0;
         e.pad = 0.0;
     }
+}
+
+// the exp/log subset from the full tables (ex[0..127] and lg are leading members of both)
+__device__ __forceinline__ void stage_glibc_exp_log(GlibcExpLog *lds, const GlibcTables *__restrict__ g) {
+    for (int i = threadIdx.x; i < 128; i += blockDim.x) {
+        lds->ex[i] = g->ex[i];
+        lds->lg[i] = g->lg[i];
+    }
+    __syncthreads();
 }
 
 __device__ __forceinline__ void stage_glibc_tables(GlibcTables *lds, const GlibcTables *__restrict__ g) {
@@ -130,7 +146,8 @@ __host__ __device__ __forceinline__ double g_exp(double x, const GlibcTables &T)
 }
 
 // glibc log(x) for positive normal finite x (the box-plus only needs x in [1, 2]).
-__host__ __device__ __forceinline__ double g_log(double x, const GlibcTables &T) {
+template <class TT>
+__host__ __device__ __forceinline__ double g_log(double x, const TT &T) {
     const uint32_t hx = g_hi(x);
     double y;
     if (hx - 0x3FEE0000u < 0x3FF10900u - 0x3FEE0000u) {
@@ -192,7 +209,8 @@ __host__ __device__ __forceinline__ double g_log(double x, const GlibcTables &T)
 // (inf/NaN) or the overflow/underflow result; 512 <= |x| < 1024 -> the main path with the
 // e_exp.c specialcase() rescaling (contraction pattern of the compiled routine: k > 0
 // fuses scale + scale*tmp, k < 0 does not, it reuses scale*tmp).
-__host__ __device__ __forceinline__ double g_exp_full(double x, const GlibcTables &T) {
+template <class TT>
+__host__ __device__ __forceinline__ double g_exp_full(double x, const TT &T) {
     const uint32_t abstop = (g_hi(x) >> 20) & 0x7FFu;
     if (abstop - 0x3C9u >= 0x3Fu) {
         if ((int)(abstop - 0x3C9u) < 0) return 1.0 + x;
@@ -241,7 +259,8 @@ __host__ __device__ __forceinline__ double g_exp_full(double x, const GlibcTable
 
 // __log_fma for every input: 0 -> -inf, +inf -> +inf, negative or NaN -> NaN, subnormals
 // rescaled by 2^52 into the main path (e_log.c special cases).
-__host__ __device__ __forceinline__ double g_log_full(double x, const GlibcTables &T) {
+template <class TT>
+__host__ __device__ __forceinline__ double g_log_full(double x, const TT &T) {
     uint32_t hx = g_hi(x), lx = g_lo(x);
     if (hx - 0x3FEE0000u < 0x3FF10900u - 0x3FEE0000u) return g_log(x, T);
     const uint32_t top = hx >> 16;

@@ -35,6 +35,7 @@ struct ProfScope {
     std::string name_;
     hipStream_t s_;
     hipEvent_t a_ = nullptr, b_ = nullptr;
+    bool capture_ = false;  // recorded into a graph being captured (external event-record nodes)
 };
 bool profiling_on();
 
@@ -60,6 +61,7 @@ int launch_transpose_to_fi_u8(int B, int ld, int64_t n, const uint8_t *src, uint
 int launch_transpose_to_fi_i64(int B, int ld, int64_t n, const int64_t *src, int64_t *dst, hipStream_t s);
 
 extern std::atomic<int> g_demap_fast;  // demap.hip (tuning knob "demap_fast")
+extern std::atomic<int> g_demap_hyp;   // demap.hip (tuning knob "demap_hyp")
 
 struct DeviceGuard {
     explicit DeviceGuard(int dev) {

@@ -237,36 +237,44 @@ QR_HD double search_replay(const SearchCmp &cmp) {
 // bracket [L, L + g] is the grid cell holding ystar.  Only its ends can lie within W of
 // ystar (every other mid is >= g - W away), and only an end that moved (L != lo,
 // H != hi) was a mid: at most one exact evaluation, whose answer shifts the cell by g.
-QR_HD double search_replay_closed(const SearchCmp &cmp) {
+// The closed form split in two, so that a wavefront can evaluate its lanes' exact F_Y
+// together (demap.hip k_demap_hyp): search_closed_prepare runs the bracket and locates the
+// final cell [L, H]; need = 1 / 2 when the end L / H lies within W of ystar and must be
+// decided exactly (at most one per search, see above), 0 when the cell is certain.  Returns
+// false when the closed form does not apply (then the general loop, search_replay, runs).
+// search_closed_finish applies the exact answer gt = (F_Y(end) > T).
+QR_HD bool search_closed_prepare(const SearchCmp &cmp, double &L, double &H, int &need) {
     double lo, hi;
     const int guard = search_bracket(cmp, lo, hi);
     const double width = hi - lo;
-    if (!(width > 1e-9) || !(width <= 0x1p20) || !(cmp.W < 0x1p-31)) {
-        double l = lo, h = hi;                    // general loop (not reached in practice)
-        int gd = guard;
-        while ((h - l) > 1e-9) {
-            if (++gd > kSearchCap) { l = h = NAN; break; }
-            const double mid = (h + l) / 2;
-            int c = cmp.quick(mid);
-            if (c == 2) c = cmp.exact(mid);
-            if (c > 0) h = mid; else l = mid;
-        }
-        return (h + l) / 2;
-    }
-    if (guard + ilogb(width) + 30 > kSearchCap) return NAN;
+    need = 0;
+    if (!(width > 1e-9) || !(width <= 0x1p20) || !(cmp.W < 0x1p-31)) return false;
+    if (guard + ilogb(width) + 30 > kSearchCap) { L = H = NAN; return true; }
     constexpr double g = 0x1p-30;
     double j = floor((cmp.ystar - lo) * 0x1p30);
     j = fmin(fmax(j, 0.0), width * 0x1p30 - 1.0);
-    double L = lo + j * g;                        // exact (|L| < 2^22)
+    L = lo + j * g;                               // exact (|L| < 2^22)
     L = (L > cmp.ystar && L > lo) ? L - g : L;    // fix the rounding of j (exact compares)
     L = (L + g <= cmp.ystar && L + g < hi) ? L + g : L;
-    double H = L + g;
-    if (L != lo && cmp.ystar - L <= cmp.W) {
-        if (cmp.exact(L) > 0) { H = L; L -= g; }  // F_Y(L) > T: hi = L
-    } else if (H != hi && H - cmp.ystar <= cmp.W) {
-        if (!(cmp.exact(H) > 0)) { L = H; H += g; }   // else lo = H
-    }
+    H = L + g;
+    if (L != lo && cmp.ystar - L <= cmp.W) need = 1;
+    else if (H != hi && H - cmp.ystar <= cmp.W) need = 2;
+    return true;
+}
+
+QR_HD double search_closed_finish(double L, double H, int need, bool gt) {
+    constexpr double g = 0x1p-30;
+    if (need == 1 && gt) { H = L; L -= g; }       // F_Y(L) > T: hi = L
+    if (need == 2 && !gt) { L = H; H += g; }      // else lo = H
     return (H + L) / 2;
+}
+
+QR_HD double search_replay_closed(const SearchCmp &cmp) {
+    double L, H;
+    int need;
+    if (!search_closed_prepare(cmp, L, H, need)) return search_replay(cmp);   // general loop
+    const bool gt = need ? cmp.exact(need == 1 ? L : H) > 0 : false;
+    return search_closed_finish(L, H, need, gt);
 }
 
 QR_HD double search_target(const DemapTables &t, double n_hat, int i) {
@@ -573,18 +581,27 @@ inline void build_quantiles(const DemapTables &t, double2 *quant) {
     }
 }
 
-// x / two_s2 correctly rounded (noisemapper.pyx:512-515 divides) in three operations:
-// q0 = RN(x y) with y = RN(1/b) is within 1 ulp of x/b, r = x - b q0 is exact (fma), and
-// RN(q0 + r y) is the correctly rounded quotient (Markstein's theorem; no overflow or
-// underflow occurs for these arguments: |x| <= ~1e4, b = 2 sigma^2 > 0 normal), except that
-// x = -0 gives +0 (harmless: the quotient only feeds exp, exp(+-0) = 1).  Pinned on
-// the host against the IEEE division (tests/native/division_check.cpp) and on the GPU by
-// the bit-exact demap tests.  The device's IEEE division is a ~10-instruction sequence
+// x / two_s2 correctly rounded (noisemapper.pyx:512-515 divides) in five operations, with
+// y = RN(1/b), b = two_s2:
+//   q0 = RN(x y)                  relative error <= 2^-52 (1+2^-53): within 2 ulp of x/b (near a
+//                                 power of two a relative 2^-52 is 2 ulp, so q0 need not be
+//                                 faithful)
+//   q1 = RN(q0 + RN(x - b q0) y)  the residual step: |x/b - q0 - r0 y| <= |x/b - q0| 2^-52
+//                                 (+ the residual's own rounding), so q1 lies within
+//                                 0.5 + 2^-50 ulp of x/b: faithful
+//   q2 = RN(q1 + (x - b q1) y)    Markstein's theorem (y within half an ulp of 1/b, q1 faithful,
+//                                 so x - b q1 is exact in one fma): the correctly rounded x/b.
+// No overflow or underflow occurs for these arguments (|x| <= ~1e4, b = 2 sigma^2 > 0 normal),
+// except that x = -0 gives +0 (harmless: the quotient only feeds exp, exp(+-0) = 1).  Pinned on
+// the host against the IEEE division (tests/native/division_check.cpp: random, near-2 quotient
+// significands, the configured 2 sigma^2 of 2..16-PAM at 0..40 dB) and on the GPU by the
+// bit-exact demap tests.  The device's IEEE division is a ~10-instruction sequence
 // (v_div_scale x2, v_rcp, fmas, v_div_fmas, v_div_fixup).
 QR_HD double div_two_s2(const DemapTables &t, double x) {
     const double q0 = x * t.inv_two_s2;
-    const double r = __builtin_fma(-q0, t.two_s2, x);
-    return __builtin_fma(r, t.inv_two_s2, q0);
+    const double q1 = __builtin_fma(__builtin_fma(-q0, t.two_s2, x), t.inv_two_s2, q0);
+    const double r1 = __builtin_fma(-q1, t.two_s2, x);
+    return __builtin_fma(r1, t.inv_two_s2, q1);
 }
 
 // noisemapper.pyx:450-540 for one symbol; out[k] = LAPPR of Gray bit k (LSB first).

@@ -66,12 +66,19 @@ ProfScope::ProfScope(std::string name, hipStream_t s) : name_(std::move(name)), 
         a_ = b_ = nullptr;
         return;
     }
-    (void)hipEventRecord(a_, s_);
+    // Inside a stream capture a plain record only marks a dependency; an external record
+    // becomes an event-record node of the graph, re-recorded at every replay (the pair then
+    // times the launch of the latest replay when qr_profile_query drains it).
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    capture_ = s_ && hipStreamIsCapturing(s_, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
+    if (capture_) (void)hipEventRecordWithFlags(a_, s_, hipEventRecordExternal);
+    else (void)hipEventRecord(a_, s_);
 }
 
 ProfScope::~ProfScope() {
     if (!a_) return;
-    (void)hipEventRecord(b_, s_);
+    if (capture_) (void)hipEventRecordWithFlags(b_, s_, hipEventRecordExternal);
+    else (void)hipEventRecord(b_, s_);
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_pending.push_back({name_, a_, b_});
     if (g_pending.size() > 4096) drain_pending_locked();
@@ -184,6 +191,21 @@ __global__ void __launch_bounds__(256) k_stream_copy(const u32x4 *__restrict__ s
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
         __builtin_nontemporal_store(__builtin_nontemporal_load(&src[i]), &dst[i]);
 }
+// One wave per workgroup; lane 0 alone times the spin (scalar counters), then stores with
+// an ordinary vector store.
+__global__ void __launch_bounds__(64) k_clock_probe(int64_t *__restrict__ out, int64_t ticks) {
+    if (threadIdx.x != 0) return;
+    const int64_t r0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+    const int64_t t0 = (int64_t)__builtin_amdgcn_s_memtime();
+    int64_t r1 = r0;
+    while (r1 - r0 < ticks) {
+        __builtin_amdgcn_s_sleep(4);
+        r1 = (int64_t)__builtin_amdgcn_s_memrealtime();
+    }
+    const int64_t t1 = (int64_t)__builtin_amdgcn_s_memtime();
+    out[2 * blockIdx.x] = t1 - t0;
+    out[2 * blockIdx.x + 1] = r1 - r0;
+}
 }  // namespace qr
 
 extern "C" {
@@ -245,6 +267,14 @@ int qr_stream_copy(const void *src, void *dst, int64_t bytes, void *st) {
     const int64_t n = bytes / 16;
     const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 256 * 64);
     qr::k_stream_copy<<<grid, 256, 0, (hipStream_t)st>>>((const qr::u32x4 *)src, (qr::u32x4 *)dst, n);
+    QR_LAUNCH_CHECK();
+    return QR_OK;
+}
+
+int qr_clock_probe(int64_t *d_out, int32_t n, int64_t realtime_ticks, void *st) {
+    if (!d_out || n <= 0 || n > 4096 || realtime_ticks <= 0 || realtime_ticks > 100000000)
+        return qr::set_error(QR_EVALUE, "qr_clock_probe: need d_out, 0 < n <= 4096, 0 < ticks <= 1e8");
+    qr::k_clock_probe<<<(unsigned)n, 64, 0, (hipStream_t)st>>>(d_out, realtime_ticks);
     QR_LAUNCH_CHECK();
     return QR_OK;
 }

@@ -62,6 +62,7 @@ SIGNATURES = {
     "qr_to_frame_innermost_u8": [i32, i32, i64, vp, vp, vp],
     "qr_to_frame_innermost_i64": [i32, i32, i64, vp, vp, vp],
     "qr_stream_copy": [vp, vp, i64, vp],
+    "qr_clock_probe": [vp, i32, i64, vp],
 }
 _RESTYPE = {"qr_last_error": C.c_char_p}
 

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""A/B of the demapper kernels on the GPU: hypothesis-parallel (demap_hyp=1, default)
+vs one lane per symbol (demap_hyp=0), both with the fast root search, at the bench's
+batch (B = 4096 frames, N = 64800): ms per launch (hipEvents, median of reps) and
+bit-identity of the LAPPRs.   python scripts/demap_ab.py [--batch 4096] [--reps 3]"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "qam-reconciliation_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--cases", default="2:3.0,2:9.5,4:13.0,4:14.5,4:25.0")
+    args = ap.parse_args()
+    import torch
+    import qamr
+    from qamr import _lib, codes
+    from qamr.pipeline import SofteningPipeline
+
+    vid, cid = codes.dvbs2_like_half()
+    dec = qamr.Decoder(vid, cid)
+    rows = []
+    for case in args.cases.split(","):
+        bps, snr = int(case.split(":")[0]), float(case.split(":")[1])
+        pipe = SofteningPipeline(dec, bps, snr, batch=args.batch, max_iterations=1)
+        b = pipe.generate(torch.Generator(device="cuda").manual_seed(0))
+        out, ms = {}, {}
+        for hyp in (1, 0):
+            _lib.tune_set("demap_hyp", hyp)
+            o = pipe.demap(b)  # warm
+            t = []
+            for _ in range(args.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                pipe.demap(b, out=o)
+                e1.record()
+                torch.cuda.synchronize()
+                t.append(e0.elapsed_time(e1))
+            ms[hyp] = sorted(t)[len(t) // 2]
+            out[hyp] = o
+        _lib.tune_set("demap_hyp", 1)
+        same = torch.equal(out[0].view(torch.int64), out[1].view(torch.int64))
+        r = {"bps": bps, "snr": snr, "B": b.B, "hyp_ms": round(ms[1], 3), "per_symbol_ms": round(ms[0], 3),
+             "speedup": round(ms[0] / ms[1], 3), "bit_identical": same}
+        rows.append(r)
+        print(json.dumps(r), flush=True)
+        del pipe, b, out
+        torch.cuda.empty_cache()
+    if not all(r["bit_identical"] for r in rows):
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

@@ -186,3 +186,46 @@ def test_fast_root_search_bit_identical_to_brute_force(gpu, bps, snr):
     a, b = fast.cpu().numpy(), brute.cpu().numpy()
     same = (a.view(np.int64) == b.view(np.int64)) | (np.isnan(a) & np.isnan(b))
     assert same.all(), f"{(~same).sum()} LAPPRs differ"
+
+
+@pytest.mark.parametrize("bps,snr", [(1, 2.0), (2, 3.0), (3, 9.5), (4, 13.0), (4, 25.0), (5, 20.0), (6, 30.0)])
+def test_hypothesis_parallel_demap_equals_per_symbol(gpu, bps, snr):
+    """The hypothesis-parallel demapper (default on 64-frame tiles: one lane per (frame,
+    hypothesis), cooperative exact F_Y, LDS combine over i) returns the per-symbol
+    kernel's doubles bit for bit, on a ragged batch (B < ld) with out-of-range symbol
+    indices (-> NaN) and both sign configurations; and its 2..16-PAM output matches the
+    oracle (reference restatement) on sampled frames."""
+    import torch
+    from qamr import _lib
+
+    pa = __import__("qamr").PAMAlphabet(bps, 2.0)
+    nv = pa.variance * 10 ** (-snr / 10) / 2
+    M = 1 << bps
+    rng = np.random.default_rng(700 + bps)
+    cfg = rng.integers(0, 2, M).astype(np.uint8)
+    nm = _nm(bps, nv, cfg)
+    S, ld, B = 257, 192, 131
+    n = rng.random((S, ld))
+    n[0, :5] = [0.0, 1.0, 1e-300, 1 - 1e-16, 0.5]
+    x = rng.integers(0, M, (S, ld))
+    x[1, :3] = [-1, M, 1 << 40]
+    dev = torch.device("cuda", 0)
+    nt = torch.from_numpy(n).to(dev).contiguous()
+    xt = torch.from_numpy(x).to(dev).contiguous()
+    try:
+        _lib.tune_set("demap_hyp", 1)
+        hyp = nm.demap_device(nt, xt, B, alpha=0.5).clone()
+        _lib.tune_set("demap_hyp", 0)
+        per = nm.demap_device(nt, xt, B, alpha=0.5).clone()
+    finally:
+        _lib.tune_set("demap_hyp", 1)
+    torch.cuda.synchronize()
+    a, b = hyp[:, :B].cpu().numpy(), per[:, :B].cpu().numpy()
+    same = (a.view(np.int64) == b.view(np.int64)) | (np.isnan(a) & np.isnan(b))
+    assert same.all(), f"{(~same).sum()} LAPPRs differ"
+    assert np.isnan(a[bps:2 * bps, :3]).all()
+    if bps <= 4:
+        onm = O.OracleNoiseMapper(bps, 2.0, nv, cfg)
+        for f in (0, 63, 64, B - 1):
+            ref = onm.demap_lappr_array(n[2:, f].copy(), x[2:, f].copy()) * 0.5
+            assert_bit_exact(a[2 * bps:, f], ref)
