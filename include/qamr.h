@@ -59,6 +59,10 @@ QR_API int qr_device_count(int32_t *count);
  * price the dominant kernel).  Off by default; zero cost when off. */
 QR_API int qr_profile_enable(int32_t on);
 QR_API int qr_profile_reset(void);
+/* Restrict the timing to the launches whose profile name is in the comma-separated list
+ * `names` (NULL or "" = every launch): the events of the other launches are not recorded
+ * at all, so timing only the kernel being priced perturbs the stream less. */
+QR_API int qr_profile_select(const char *names);
 /* name: "check" (one check sweep, all degree classes), "check_d<D>" (the launch
  * for check degree D), "check1" (first sweep), "var", "var_init", "status",
  * "parity", "demap", "bob", "syndrome", "count".  Synchronises pending events. */

@@ -1099,6 +1099,57 @@ static int run_split2(const Plan &P, int max_it) {
     return QR_OK;
 }
 
+// Two independent pipelines (split = 4): the frame halves A and B share no data, so each
+// runs its own in-order sequence  C(1) | V(1) C(2) S(1) | V(2) C(3) S(2) | ...  on its own
+// stream (A on the caller's, B on the second), with no cross-stream event inside the loop:
+// the GPU interleaves the two, and one half's launch tail is filled by the other half's
+// work instead of an event wait.  Per frame the order is exactly run_split's.
+static int run_pipes(const Plan &P, int max_it) {
+    const qr_code *code = P.code;
+    std::lock_guard<std::mutex> lk(code->mu);
+    if (!code->s2) {  // first use: all or nothing
+        hipStream_t s2 = nullptr;
+        hipEvent_t ev[5] = {};
+        hipError_t e = hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
+        for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+        if (e != hipSuccess) {
+            for (auto x : ev)
+                if (x) (void)hipEventDestroy(x);
+            if (s2) (void)hipStreamDestroy(s2);
+            return set_error(QR_EDEVICE, "decode: second stream: %s", hipGetErrorString(e));
+        }
+        for (int i = 0; i < 5; ++i) code->ev[i] = ev[i];
+        code->s2 = s2;
+    }
+    hipEvent_t fork = code->ev[0], join = code->ev[4];
+    const int ld = P.ld, h = ld / 2;
+    auto row = [&](int t) { return P.w.unsat + (size_t)t * ld; };
+    Plan PB = P;
+    PB.s = code->s2;
+    QR_HIP(hipEventRecord(fork, P.s));
+    QR_HIP(hipStreamWaitEvent(PB.s, fork, 0));
+    int rc;
+    for (int half = 0; half < 2; ++half) {
+        const Plan &Q = half ? PB : P;
+        const int f0 = half ? h : 0, f1 = half ? ld : h;
+        if ((rc = launch_checks<kFirst>(Q, P.post, row(0), f0, f1))) return rc;
+    }
+    for (int t = 1; t <= max_it; ++t) {
+        for (int half = 0; half < 2; ++half) {   // enqueue order only: the streams run freely
+            const Plan &Q = half ? PB : P;
+            const int f0 = half ? h : 0, f1 = half ? ld : h;
+            if ((rc = launch_var<false>(Q, f0, f1))) return rc;
+            if (t < max_it) {
+                if ((rc = launch_checks<kNormal>(Q, P.post, row(t), f0, f1))) return rc;
+                if ((rc = launch_status_compact(Q, f0, f1, t, row(t)))) return rc;
+            }
+        }
+    }
+    QR_HIP(hipEventRecord(join, PB.s));
+    QR_HIP(hipStreamWaitEvent(P.s, join, 0));
+    return QR_OK;
+}
+
 int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr, const uint8_t *synd, int max_it,
                         double *final_post, uint8_t *success, int32_t *iters, void *ws_ptr, size_t ws_size,
                         hipStream_t s) {
@@ -1143,7 +1194,9 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     } else if ((rc = launch_compact(P, 0, ld))) {
         return rc;
     }
-    if ((rc = !split ? run_flat(P, max_it) : sp >= 3 ? run_split2(P, max_it) : run_split(P, max_it))) return rc;
+    if ((rc = !split ? run_flat(P, max_it) : sp >= 4 ? run_pipes(P, max_it) : sp == 3 ? run_split2(P, max_it)
+                                                                           : run_split(P, max_it)))
+        return rc;
     // Check after the last sweep; then every frame still running stops with (0, max).
     const int tf = max_it > 0 ? max_it : 0;
     uint8_t *unsat_last = P.w.unsat + (size_t)tf * ld;

@@ -21,8 +21,11 @@ namespace qr {
 
 // 1 = Newton-located root + replayed bisection (bit-identical, ~5x fewer erf), 0 = brute force.
 std::atomic<int> g_demap_fast{1};
-// 1 = hypothesis-parallel kernel (k_demap_hyp) on 64-frame tiles, 0 = one lane per symbol (k_demap).
+// Demap kernel on 64-frame tiles: 0 = one lane per symbol (k_demap), 2 = hypothesis-parallel
+// (k_demap_hyp) for every order, 1 (default) = hypothesis-parallel from 16-PAM up (measured on
+// MI355X, B = 4096: 16-PAM 46.8 vs 47.1 ms with no scratch traffic; 4-PAM 20.0 vs 13.9 ms).
 std::atomic<int> g_demap_hyp{1};
+constexpr int kDemapHypAutoBps = 4;
 
 #ifndef QR_DEMAP_WAVES
 // Single-loop LLR sum: 5 waves/SIMD (96 VGPRs, 52-84 B spilled) 53.4 / 58.5 ms vs 4 waves 55.9 / 62.5 ms
@@ -77,6 +80,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QR_DEM
 // per resident workgroup.
 constexpr int kDemapHypWaves = 4;
 constexpr int kDemapHypMaxBps = 6;
+#ifndef QR_DEMAP_EXPW
+#define QR_DEMAP_EXPW 1      // LLR-sum exp: glibc main path branch-free, specials per wave (g_exp_wave)
+#endif
+#ifndef QR_DEMAP_HYP_UNROLL
+#define QR_DEMAP_HYP_UNROLL 4
+#endif
+#ifndef QR_DEMAP_HYP_EU
+#define QR_DEMAP_HYP_EU 1    // amdgpu_waves_per_eu floor of k_demap_hyp (1 = the compiler's choice)
+#endif
 
 // rank of this lane among the set lanes of mk below it
 __device__ __forceinline__ int lane_rank(uint64_t mk) {
@@ -128,7 +140,8 @@ __device__ __forceinline__ double g_inv_search_wave(const DemapTables &t, const 
 }
 
 template <int BPS>
-__global__ void __launch_bounds__(64 * kDemapHypWaves) k_demap_hyp(const DemapTables *__restrict__ tab,
+__global__ void __launch_bounds__(64 * kDemapHypWaves) __attribute__((amdgpu_waves_per_eu(QR_DEMAP_HYP_EU, 8)))
+k_demap_hyp(const DemapTables *__restrict__ tab,
                                                                   const MathTables *__restrict__ gmt, int B, int ld,
                                                                   int64_t S, const double *__restrict__ n,
                                                                   const int64_t *__restrict__ j, double alpha,
@@ -160,11 +173,18 @@ __global__ void __launch_bounds__(64 * kDemapHypWaves) k_demap_hyp(const DemapTa
             // noisemapper.pyx:503-515 in the reference's summation order (k < j, p[j], k > j)
             // as one loop with the argument selected per lane (see demap_symbol)
             double sum = 0;
-#pragma unroll 4
+#pragma unroll QR_DEMAP_HYP_UNROLL
             for (int k = 0; k < M; ++k) {
                 const double e = (2 * y - t.a[k] - aj) * (t.a[k] - aj);
-                const double arg = k < jj ? e : div_two_s2(t, e);
-                const double term = k == jj ? t.p[jj] : g_exp_full(arg, gt) * t.p[k];
+                // (k == j: the term is p[j]; its exp argument, 0, would send the wave down the
+                // special-case path of g_exp_wave for nothing)
+                const double arg = k < jj ? e : k == jj ? 1.0 : div_two_s2(t, e);
+#if QR_DEMAP_EXPW
+                const double ex = g_exp_wave(arg, gt);
+#else
+                const double ex = g_exp_full(arg, gt);
+#endif
+                const double term = k == jj ? t.p[jj] : ex * t.p[k];
                 sum += term;
             }
             q[i][lane] = t.dF[i] / sum;
@@ -401,7 +421,9 @@ int demap_batch_device(const qr_demap *dm, int B, int ld, int64_t S, const doubl
     DeviceGuard g(dm->device);
     ProfScope ps("demap", s);
     const bool fast = g_demap_fast.load() != 0;
-    if (fast && g_demap_hyp.load() != 0 && ld % kWave == 0 && dm->h.bps <= kDemapHypMaxBps) {
+    const int hyp = g_demap_hyp.load();
+    if (fast && (hyp >= 2 || (hyp == 1 && dm->h.bps >= kDemapHypAutoBps)) && ld % kWave == 0 &&
+        dm->h.bps <= kDemapHypMaxBps) {
         const int64_t items = S * (ld / kWave);
         launch_demap_hyp(dm->h.bps, demap_hyp_grid(dm->device, items), s, dm, B, ld, S, n, j, alpha, lappr);
     } else {

@@ -257,6 +257,36 @@ __host__ __device__ __forceinline__ double g_exp_full(double x, const TT &T) {
     return y * 0x1p-1022;
 }
 
+// g_exp_full with its special cases kept off the common path: glibc's main path (|x| in
+// [2^-54, 512), e_exp.c:90-140 without specialcase) runs branch-free on every lane, and only
+// when some lane of the wavefront has an argument outside that range does the wave run
+// g_exp_full for those lanes (one wave-uniform branch instead of two per-lane ones and their
+// exec-mask bookkeeping).  Same bits as g_exp_full for every input.
+template <class TT>
+__device__ __forceinline__ double g_exp_wave(double x, const TT &T) {
+    const uint32_t abstop = (g_hi(x) >> 20) & 0x7FFu;
+    const bool special = abstop - 0x3C9u >= 0x408u - 0x3C9u;
+    double kd = __builtin_fma(x, kGxInvLn2N, kGxShift);
+    const uint32_t ki = g_lo(kd);
+    kd = kd - kGxShift;
+    double r = __builtin_fma(kd, kGxNegLn2hiN, x);
+    r = __builtin_fma(kd, kGxNegLn2loN, r);
+    const double2 e = T.ex[ki & 127u];
+    const double scale = g_make(g_add_ki(g_hi(e.y), ki), g_lo(e.y));
+    const double r2 = r * r;
+    const double p23 = __builtin_fma(r, kGxC3, kGxC2);
+    const double tr = e.x + r;
+    const double p45 = __builtin_fma(r, kGxC5, kGxC4);
+    const double a = __builtin_fma(p23, r2, tr);
+    const double r4 = r2 * r2;
+    const double tmp = __builtin_fma(r4, p45, a);
+    double res = __builtin_fma(scale, tmp, scale);
+    if (__builtin_amdgcn_ballot_w64(special)) {   // wave-uniform
+        if (special) res = g_exp_full(x, T);
+    }
+    return res;
+}
+
 // __log_fma for every input: 0 -> -inf, +inf -> +inf, negative or NaN -> NaN, subnormals
 // rescaled by 2^52 into the main path (e_log.c special cases).
 template <class TT>

@@ -130,6 +130,7 @@ inline int build_demap_host(int32_t bps, const double *constellation, const doub
     for (int i = 1; i < M; ++i) t.Fthr[i] = single_F_Y(t, t.thr[i]);
     for (int i = 0; i < M; ++i) t.dF[i] = t.Fthr[i + 1] - t.Fthr[i];  // :159-162
     t.inv_den = 1.0 / t.den;
+    for (int i = 0; i < M; ++i) t.inv_dF[i] = 1.0 / t.dF[i];          // Newton start only
     t.amin = t.amax = t.a[0];
     for (int i = 1; i < M; ++i) {
         t.amin = fmin(t.amin, t.a[i]);

@@ -36,6 +36,7 @@ struct ProfScope {
     hipStream_t s_;
     hipEvent_t a_ = nullptr, b_ = nullptr;
     bool capture_ = false;  // recorded into a graph being captured (external event-record nodes)
+    void record(hipEvent_t e);
 };
 bool profiling_on();
 

@@ -121,6 +121,7 @@ struct DemapTables {
     double thr[kMaxOrder + 1];  // decision thresholds
     double Fthr[kMaxOrder + 1]; // F_Y_thresholds
     double dF[kMaxOrder];       // delta_F_Y
+    double inv_dF[kMaxOrder];   // 1 / delta_F_Y (Newton start only: never decides a comparison)
     uint8_t sign[kMaxOrder];    // sign_config
     double inv_den;             // 1 / den (Newton only)
     double amin, amax;          // constellation extremes (Newton window bound)
@@ -216,6 +217,29 @@ QR_HD int search_bracket(const SearchCmp &cmp, double &lo, double &hi) {
     return guard;
 }
 
+// search_bracket in closed form when the window is certified: the loop probes 2^m (up) or
+// -2^m (down), m = 0, 1, ..., and stops at the first probe quick() does not place on the
+// near side of ystar.  With z = ystar (up) or -ystar (down), that is m* = 0 if z + W < 1,
+// else ilogb(z + W) + 1 -- verified with the loop's own comparisons at 2^m* and 2^(m*-1)
+// (quick() is monotone in the probe, so the smaller probes agree with 2^(m*-1)); any probe
+// inside the window, or a rounding that breaks the verification, takes the loop.  Same
+// lo, hi and guard as the loop, ~20 instructions instead of ~20 per doubling.
+QR_HD int search_bracket_fast(const SearchCmp &cmp, double &lo, double &hi) {
+    if (!cmp.have) return search_bracket(cmp, lo, hi);
+    const bool up = cmp.T > .5;
+    const double z = up ? cmp.ystar : -cmp.ystar;
+    const double x = z + cmp.W;
+    const int m = (x < 1.0) ? 0 : ilogb(x) + 1;
+    if (!(m >= 0 && m <= 1000)) return search_bracket(cmp, lo, hi);
+    const double p = ldexp(1.0, m), q = (m > 0) ? ldexp(1.0, m - 1) : 0.0;
+    const double stop = up ? p : -p, prev = up ? q : -q;
+    const int want = up ? 1 : -1;   // the stopping probe: F(2^m) > T (up) / F(-2^m) < T (down)
+    if (cmp.quick(stop) != want || (m > 0 && cmp.quick(prev) != -want)) return search_bracket(cmp, lo, hi);
+    lo = up ? q : -p;
+    hi = up ? p : -q;
+    return m;
+}
+
 // The reference's bracket + bisection (noisemapper.pyx:314-345) on a comparison oracle.
 QR_HD double search_replay(const SearchCmp &cmp) {
     double lo, hi;
@@ -245,7 +269,7 @@ QR_HD double search_replay(const SearchCmp &cmp) {
 // search_closed_finish applies the exact answer gt = (F_Y(end) > T).
 QR_HD bool search_closed_prepare(const SearchCmp &cmp, double &L, double &H, int &need) {
     double lo, hi;
-    const int guard = search_bracket(cmp, lo, hi);
+    const int guard = search_bracket_fast(cmp, lo, hi);
     const double width = hi - lo;
     need = 0;
     if (!(width > 1e-9) || !(width <= 0x1p20) || !(cmp.W < 0x1p-31)) return false;
@@ -388,7 +412,7 @@ QR_HD double hermite(double2 n0, double2 n1, double x) {
 // Start point for the root of F_Y(y) = T in region k; NaN when out of the table.
 QR_HD double quantile_start(const DemapTables &t, int k, double T) {
     const double2 *Qk = t.quant + (size_t)k * kQStride;
-    const double u = (T - t.Fthr[k]) / t.dF[k];
+    const double u = (T - t.Fthr[k]) * t.inv_dF[k];
     const double w = (u < 0.5) ? u : 1.0 - u;
     if (w < 1.0 / (1 << kZoneOct)) {
         const double x = (log2(w) + kZoneDepth) * kPerOct;
@@ -404,6 +428,20 @@ QR_HD double quantile_start(const DemapTables &t, int k, double T) {
     if (i < 0) i = 0;
     if (i > kMid - 1) i = kMid - 1;
     return hermite(Qk[kZone + i], Qk[kZone + i + 1], x - i);
+}
+
+// 1/f for the Newton step and window: the device's v_rcp_f64 refined by two Newton-Raphson
+// steps (relative error ~2^-52, against the ~10-instruction IEEE division).  It only steers
+// the root location; the window keeps a 2^-40 relative margin for it (wf), far below the x2
+// and x4 slack of its terms.
+QR_HD double newton_recip(double f) {
+#ifdef __HIP_DEVICE_COMPILE__
+    double r = __builtin_amdgcn_rcp(f);
+    r = __builtin_fma(__builtin_fma(-f, r, 1.0), r, r);
+    return __builtin_fma(__builtin_fma(-f, r, 1.0), r, r);
+#else
+    return 1.0 / f;
+#endif
 }
 
 // Newton from the Hermite start, usually one evaluation; returns false if it cannot
@@ -433,11 +471,12 @@ QR_HD bool newton_root(const DemapTables &t, const MathTables &mt, double T, int
             F_and_density(t, mt, y, F, f, A_);
         }
         if (!(f > 0.0)) return false;
-        const double d = (F - T) / f;
+        const double rf = newton_recip(f);
+        const double d = (F - T) * rf;
         y -= d;
         const double A = fmax(fabs(y - t.amin), fabs(y - t.amax)) * t.inv_den;
         const double wn = 4.0 * (A + 1.0) * t.inv_den * d * d;
-        const double wf = ef / f + 4.0 * eps * fabs(y);
+        const double wf = ef * rf * (1.0 + 0x1p-40) + 4.0 * eps * fabs(y);
         if (fabs(d) * (A + 1.0) <= 1e-3 * t.den && wn <= fmax(wf, 1e-13)) {
             ystar = y;
             W = wn + wf;

@@ -5,6 +5,7 @@
 
 #include <atomic>
 #include <map>
+#include <set>
 
 #include "qamr_internal.hpp"
 
@@ -39,9 +40,11 @@ struct Stat {
     int64_t n = 0;
 };
 std::atomic<bool> g_prof{false};
+std::atomic<bool> g_prof_external{true};  // external event-record nodes accepted in captures
 std::mutex g_prof_mu;
 std::vector<Pending> g_pending;
 std::map<std::string, Stat> g_stats;
+std::set<std::string> g_prof_select;  // empty: every launch is timed
 
 void drain_pending_locked() {
     for (auto &p : g_pending) {
@@ -62,6 +65,10 @@ bool profiling_on() { return g_prof.load(std::memory_order_relaxed); }
 
 ProfScope::ProfScope(std::string name, hipStream_t s) : name_(std::move(name)), s_(s) {
     if (!profiling_on()) return;
+    {
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        if (!g_prof_select.empty() && !g_prof_select.count(name_)) return;
+    }
     if (hipEventCreate(&a_) != hipSuccess || hipEventCreate(&b_) != hipSuccess) {
         a_ = b_ = nullptr;
         return;
@@ -71,14 +78,21 @@ ProfScope::ProfScope(std::string name, hipStream_t s) : name_(std::move(name)), 
     // times the launch of the latest replay when qr_profile_query drains it).
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     capture_ = s_ && hipStreamIsCapturing(s_, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
-    if (capture_) (void)hipEventRecordWithFlags(a_, s_, hipEventRecordExternal);
-    else (void)hipEventRecord(a_, s_);
+    record(a_);
+}
+
+void ProfScope::record(hipEvent_t e) {
+    if (capture_ && g_prof_external.load()) {
+        if (hipEventRecordWithFlags(e, s_, hipEventRecordExternal) == hipSuccess) return;
+        (void)hipGetLastError();  // unsupported here: clear the sticky error, record plainly
+        g_prof_external.store(false);
+    }
+    (void)hipEventRecord(e, s_);
 }
 
 ProfScope::~ProfScope() {
     if (!a_) return;
-    if (capture_) (void)hipEventRecordWithFlags(b_, s_, hipEventRecordExternal);
-    else (void)hipEventRecord(b_, s_);
+    record(b_);
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_pending.push_back({name_, a_, b_});
     if (g_pending.size() > 4096) drain_pending_locked();
@@ -228,6 +242,19 @@ int qr_device_count(int32_t *count) {
 
 int qr_profile_enable(int32_t on) {
     qr::g_prof.store(on != 0);
+    return QR_OK;
+}
+
+int qr_profile_select(const char *names) {
+    std::lock_guard<std::mutex> lk(qr::g_prof_mu);
+    qr::g_prof_select.clear();
+    std::string n = names ? names : "";
+    size_t p = 0;
+    while (p <= n.size()) {
+        const size_t q = std::min(n.find(',', p), n.size());
+        if (q > p) qr::g_prof_select.insert(n.substr(p, q - p));
+        p = q + 1;
+    }
     return QR_OK;
 }
 

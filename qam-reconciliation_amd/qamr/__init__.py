@@ -7,7 +7,8 @@ There is no CPU fallback: constructing a Decoder/NoiseMapper/Matrix without a
 HIP device raises.
 """
 from . import codes
-from ._lib import QamrError, build, device_count, load, profile_enable, profile_query, profile_reset
+from ._lib import (QamrError, build, device_count, load, profile_enable, profile_query, profile_reset,
+                   profile_select)
 from .alphabet import Alphabet, PAMAlphabet, generate_table_s_to_b
 from .decoder import Decoder
 from .matrix import Matrix
@@ -16,4 +17,4 @@ from .utils import count_errors_from_lappr
 
 __all__ = ["Decoder", "Matrix", "NoiseMapper", "NoiseDemapper", "PAMAlphabet", "Alphabet", "codes",
            "count_errors_from_lappr", "generate_table_s_to_b", "build", "load", "device_count", "QamrError",
-           "profile_enable", "profile_query", "profile_reset"]
+           "profile_enable", "profile_query", "profile_reset", "profile_select"]

@@ -32,6 +32,7 @@ SIGNATURES = {
     "qr_device_count": [P(i32)],
     "qr_profile_enable": [i32],
     "qr_profile_reset": [],
+    "qr_profile_select": [C.c_char_p],
     "qr_profile_query": [C.c_char_p, P(f64), P(i64)],
     "qr_tune_set": [C.c_char_p, i64],
     "qr_tune_get": [C.c_char_p, P(i64)],
@@ -157,6 +158,14 @@ def profile_enable(on: bool = True):
 
 def profile_reset():
     check(load().qr_profile_reset())
+
+
+def profile_select(names=None):
+    """Time only the launches named in ``names`` (iterable or comma-separated string);
+    None = every launch."""
+    if names is not None and not isinstance(names, str):
+        names = ",".join(names)
+    check(load().qr_profile_select((names or "").encode()))
 
 
 def profile_query(name: str):

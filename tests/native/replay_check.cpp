@@ -38,6 +38,7 @@ int main(int argc, char** argv) {
             t.Fthr[0] = 0; t.Fthr[M] = 1;
             for (int i = 1; i < M; ++i) t.Fthr[i] = qr::single_F_Y(t, t.thr[i]);
             for (int i = 0; i < M; ++i) t.dF[i] = t.Fthr[i + 1] - t.Fthr[i];
+            for (int i = 0; i < M; ++i) t.inv_dF[i] = 1.0 / t.dF[i];
             t.inv_den = 1.0 / t.den; t.amin = t.a[0]; t.amax = t.a[M - 1];
             std::vector<double2> quant((size_t)M * qr::kQStride);
             qr::build_quantiles(t, quant.data());

@@ -26,6 +26,11 @@ def test_fast_search_bit_identical(tmp_path):
     print(run.stdout)
     assert run.returncode == 0, run.stdout
     assert "mismatches=0" in run.stdout
+    # the fast path itself must be exercised: Newton certifies ~91 % of these draws (the rest
+    # are the edge targets n = 0 / 1, 1e-12-deep tails and -2 dB spreads: brute force)
+    import re
+    m = re.search(r"draws=(\d+) mismatches=\d+ fallbacks=(\d+)", run.stdout)
+    assert m and int(m.group(2)) < 0.15 * int(m.group(1)), run.stdout
 
 
 def test_llr_exponent_division_bit_identical(tmp_path):

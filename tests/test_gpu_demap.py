@@ -190,7 +190,7 @@ def test_fast_root_search_bit_identical_to_brute_force(gpu, bps, snr):
 
 @pytest.mark.parametrize("bps,snr", [(1, 2.0), (2, 3.0), (3, 9.5), (4, 13.0), (4, 25.0), (5, 20.0), (6, 30.0)])
 def test_hypothesis_parallel_demap_equals_per_symbol(gpu, bps, snr):
-    """The hypothesis-parallel demapper (default on 64-frame tiles: one lane per (frame,
+    """The hypothesis-parallel demapper (default from 16-PAM up on 64-frame tiles: one lane per (frame,
     hypothesis), cooperative exact F_Y, LDS combine over i) returns the per-symbol
     kernel's doubles bit for bit, on a ragged batch (B < ld) with out-of-range symbol
     indices (-> NaN) and both sign configurations; and its 2..16-PAM output matches the
@@ -213,7 +213,7 @@ def test_hypothesis_parallel_demap_equals_per_symbol(gpu, bps, snr):
     nt = torch.from_numpy(n).to(dev).contiguous()
     xt = torch.from_numpy(x).to(dev).contiguous()
     try:
-        _lib.tune_set("demap_hyp", 1)
+        _lib.tune_set("demap_hyp", 2)   # hypothesis-parallel for every order
         hyp = nm.demap_device(nt, xt, B, alpha=0.5).clone()
         _lib.tune_set("demap_hyp", 0)
         per = nm.demap_device(nt, xt, B, alpha=0.5).clone()

@@ -74,7 +74,7 @@ def _dvbs2_batch(B, snr_db, seed=0):
 TUNINGS = [dict(split=1), dict(split=2, check_per=1), dict(check_ft=64, check_per=3, var_ft=128, var_per=1),
            dict(nt=0), dict(split=1, check_ft=128, var_per=16), dict(split=3), dict(split=3, lds_pad_kb=0, nt=0),
            dict(split=2), dict(compact=0), dict(split=1, compact=0), dict(split=2, compact=0), dict(side=0),
-           dict(side=0, compact=0)]
+           dict(side=0, compact=0), dict(split=4), dict(split=4, compact=0)]
 
 
 def test_schedule_and_tuning_invariance(gpu):
