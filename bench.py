@@ -279,7 +279,7 @@ def copy_bandwidth(dev, nbytes=2 << 30, reps=5):
     return gbps
 
 
-def probe_clock(w, n=8, ms=2.0):
+def probe_clock(w, n=16, ms=3.0):
     """Shader clock under the decode's load, unprofiled: one eager step is enqueued, then
     n one-wave clock probes (qr_clock_probe: shader cycles / 100 MHz realtime ticks over
     ~ms each) on a side stream, which the GPU schedules beside the step's kernels.
@@ -301,6 +301,7 @@ def probe_clock(w, n=8, ms=2.0):
         torch.cuda.synchronize(w.dev)
         o = out.cpu().numpy().reshape(n, 2)
         ghz = sorted(float(c) / float(r) * 0.1 for c, r in o if r > 0)
+        probe_clock.spread = (round(ghz[0], 3), round(ghz[-1], 3)) if ghz else None
         return ghz[len(ghz) // 2] if ghz else None
     except Exception:
         return None
@@ -374,6 +375,7 @@ def roofline(args, w, kstats, dev):
                             "clock_ghz": round(clk, 3),
                             "clock_source": "live (qr_clock_probe beside an unprofiled step)" if clk_live
                             else "profiled PMC pass" if clk_pmc else "spec",
+                            "clock_ghz_probe_min_max": getattr(probe_clock, "spread", None) if clk_live else None,
                             "clock_ghz_pmc": round(clk_pmc, 3) if clk_pmc else None,
                             "issue_ms": round(busy * 1e3, 3),
                             "frac": round(busy / avg_s, 4),

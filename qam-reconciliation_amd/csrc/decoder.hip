@@ -54,8 +54,8 @@ struct Arith {  // kFast, kEps: MathTables (10 KiB) in LDS
     }
 };
 template <>
-struct Arith<kStrict> {  // GlibcTables (10 KiB) in LDS
-    using Tab = GlibcTables;
+struct Arith<kStrict> {  // the box-plus part of GlibcTables (8 KiB) in LDS
+    using Tab = GlibcTablesBP;
     using Regs = GlibcK;
     static __device__ __forceinline__ Regs regs() { return GlibcK::pinned(); }
     static __device__ __forceinline__ double bp(double a, double b, const Tab &T, const Regs &K) {
@@ -211,6 +211,12 @@ __device__ __forceinline__ void stage_tables(typename Arith<AR>::Tab *lds, const
 #ifndef QR_PACK_PREFETCH
 #define QR_PACK_PREFETCH 0
 #endif
+// QR_CHECK_GLDS: the packed strict check sweep gathers the next check's posteriors by LDS DMA
+// (buffer_load_dword ... lds) right after it has consumed the current check's inputs, so the
+// gathers of check j+1 are in flight during the arithmetic of check j without holding VGPRs.
+#ifndef QR_CHECK_GLDS
+#define QR_CHECK_GLDS 0
+#endif
 template <int D, int MODE, bool NT>
 struct CheckIn {
     double p[D], c[D];
@@ -226,6 +232,36 @@ struct CheckIn {
         for (int i = 0; i < D; ++i) {
             p[i] = ld_row<false>(row_ptr(a.post, sld(a.chk_var + base + i), ld), b8, ld);
             if (MODE == kNormal && QR_PREFETCH_C) c[i] = ld_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), ld), b8, ld);
+        }
+    }
+    // LDS-DMA flavour (QR_CHECK_GLDS): the D gathered posterior rows go straight into this
+    // wave's LDS buffer pg (D x 128 dwords: the lanes' low dwords, then their high dwords,
+    // row after row -- buffer_load_dword ... lds writes lane-linear), no VGPR holds them
+    // in flight; the syndrome byte stays an ordinary load.
+    __device__ __forceinline__ void load_glds(const CheckArgs &a, int64_t ci, int f, uint32_t *pg) {
+        const int ld = a.ld;
+        const uint32_t b8 = (uint32_t)f * 8u;
+        const int cc = sld(a.checks + ci);
+        base = sld(a.chk_ptr + cc);
+        sb = *at_byte(row_ptr(a.synd, cc, ld), (uint32_t)f);
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            const __amdgpu_buffer_rsrc_t r = row_rsrc(row_ptr(a.post, sld(a.chk_var + base + i), ld), ld);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)(pg + i * 128), 4,
+                                                    b8, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)(pg + i * 128 + 64),
+                                                    4, b8 + 4u, 0, 0, 0);
+        }
+    }
+    // Wait for the DMA (the compiler does not track it: an explicit vmcnt(0), which is also a
+    // compiler memory barrier so the LDS reads stay below it), then read back.
+    __device__ __forceinline__ void read_glds(const uint32_t *pg) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t lane = __lane_id();
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            const uint32_t *q = pg + i * 128;
+            p[i] = __builtin_bit_cast(double, ((uint64_t)q[64 + lane] << 32) | q[lane]);
         }
     }
     __device__ __forceinline__ void load_c(const CheckArgs &a, int f) {
@@ -336,9 +372,10 @@ __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m
 // VALU instructions) in every lane whose inputs are all in its domain, the exact path
 // in the others; a wave whose lanes agree runs one path only (the other is skipped
 // under an empty exec mask), and a frame's result never depends on its wave-mates.
-template <int D, int MODE, bool NT, int AR, bool FIN = false>
+template <int D, int MODE, bool NT, int AR, bool FIN = false, bool GL = false>
 __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, unsigned by,
-                                            const typename Arith<AR>::Tab &tab, double *hb) {
+                                            const typename Arith<AR>::Tab &tab, double *hb,
+                                            uint32_t *pgb = nullptr) {
     const int ft = 1 << a.g.lft;
     const int nsub = 256 >> a.g.lft;
     const int ld = a.ld;
@@ -402,9 +439,12 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
         return;
     }
     CheckIn<D, MODE, NT> nx;
-    nx.load(a, ci, f);
+    uint32_t *pg = GL ? pgb + (threadIdx.x >> 6) * (D * 128) : nullptr;
+    if constexpr (GL) nx.load_glds(a, ci, f, pg);
+    else nx.load(a, ci, f);
     for (int j = 0; j < a.g.per; ++j) {
         // consume check j's inputs (m, parity) before its registers take check j+1's
+        if constexpr (GL) nx.read_glds(pg);
         nx.load_c(a, f);
         uint32_t par = nx.sb;
         double m[D];
@@ -418,7 +458,11 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
         struct { int base; uint8_t sb; } cur = {nx.base, nx.sb};
         const int64_t cn = ci + nsub;
         const bool more = (j + 1 < a.g.per) && cn < a.n_checks;   // wave-uniform
-        if (kPrefetch && more) nx.load(a, cn, f);
+        if constexpr (GL) {
+            if (more) nx.load_glds(a, cn, f, pg);   // the reads above have completed (m uses them)
+        } else if (kPrefetch && more) {
+            nx.load(a, cn, f);
+        }
         if (MODE != kFirst) bad |= (par == 1u) ? 1u : 0u;  // satisfied iff (parity ^ 1) != 0
         if (MODE != kParityOnly) {
             const uint32_t b8 = (uint32_t)f * 8u;
@@ -440,7 +484,7 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
             }
         }
         if (!more) break;
-        if (!kPrefetch) nx.load(a, cn, f);
+        if (!kPrefetch && !GL) nx.load(a, cn, f);
         ci = cn;
     }
     if (MODE != kFirst && bad && act && live) a.unsat[f] = 1;  // benign race: every writer stores 1
@@ -481,17 +525,19 @@ __device__ __forceinline__ void var_block(const VarArgs &a, unsigned bx, unsigne
 template <int D, int MODE, bool NT, int AR>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AR == kStrict ? QR_CHECK_STRICT_WAVES : 1, 8)))
 k_check(CheckArgs a) {
+    constexpr bool GL = QR_CHECK_GLDS && AR == kStrict && QR_STRICT_PACK && D <= kPackMaxDeg;
     __shared__ typename Arith<AR>::Tab tab;
     __shared__ double hb[PackLds<AR>::doubles];
+    __shared__ uint32_t pgb[GL ? 4 * D * 128 : 1];   // 4 waves x D posterior rows (LDS DMA)
     if (!frames_block_live(a.acount, blockIdx.y, a.g.lft)) return;  // block-uniform
     if (MODE != kParityOnly) stage_tables<AR>(&tab, a);
     if constexpr (AR == kStrict && MODE != kParityOnly && QR_STRICT_FINITE && QR_STRICT_PACK && D <= kPackMaxDeg) {
         if (a.finite && sld(a.finite)) {  // kernel-uniform: one of the two bodies runs
-            check_block<D, MODE, NT, AR, true>(a, blockIdx.x, blockIdx.y, tab, hb);
+            check_block<D, MODE, NT, AR, true, GL>(a, blockIdx.x, blockIdx.y, tab, hb, pgb);
             return;
         }
     }
-    check_block<D, MODE, NT, AR>(a, blockIdx.x, blockIdx.y, tab, hb);
+    check_block<D, MODE, NT, AR, false, GL>(a, blockIdx.x, blockIdx.y, tab, hb, pgb);
 }
 
 // finite = 1 iff every LAPPR of frames [0, B) is below bound in magnitude (the flag was set

@@ -61,9 +61,17 @@ struct GlibcLogK {
 // (one instruction instead of an and + shift); glibc's own index ki % 128 reads the same data.
 struct GlibcTables {
     double2 ex[256];
+    GlibcLogK lk[128];
     double2 lg[128];
+};
+// The box-plus' part of GlibcTables (its leading 8 KiB: ex and lk): what the strict check
+// sweep stages in LDS (g_exp_neg, g_log_table, h_packed read nothing else).
+struct GlibcTablesBP {
+    double2 ex[256];
     GlibcLogK lk[128];
 };
+static_assert(sizeof(GlibcTablesBP) == 8192, "box-plus tables: 8 KiB");
+static_assert(offsetof(GlibcTables, lk) == offsetof(GlibcTablesBP, lk), "GlibcTablesBP is a prefix of GlibcTables");
 
 // The demapper's subset (glibc_math g_exp_full / g_log_full read only ex[ki % 128] and lg):
 // 4 KiB of LDS per workgroup instead of 10.
@@ -98,10 +106,11 @@ __device__ __forceinline__ void stage_glibc_exp_log(GlibcExpLog *lds, const Glib
     __syncthreads();
 }
 
-__device__ __forceinline__ void stage_glibc_tables(GlibcTables *lds, const GlibcTables *__restrict__ g) {
+template <class TT>   // GlibcTables or its prefix GlibcTablesBP
+__device__ __forceinline__ void stage_glibc_tables(TT *lds, const GlibcTables *__restrict__ g) {
     const double2 *src = reinterpret_cast<const double2 *>(g);
     double2 *dst = reinterpret_cast<double2 *>(lds);
-    constexpr int n = sizeof(GlibcTables) / sizeof(double2);
+    constexpr int n = sizeof(TT) / sizeof(double2);
     for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
     __syncthreads();
 }
@@ -126,7 +135,8 @@ __host__ __device__ __forceinline__ uint32_t g_add_ki(uint32_t hi, uint32_t ki) 
 // glibc exp(x) for |x| < 512 (finite; NaN propagates).  The table index and the
 // exponent come from the low word of kd (|ki| < 2^17, so ki << 45 only touches the
 // high word of sbits).
-__host__ __device__ __forceinline__ double g_exp(double x, const GlibcTables &T) {
+template <class TT>
+__host__ __device__ __forceinline__ double g_exp(double x, const TT &T) {
     double kd = __builtin_fma(x, kGxInvLn2N, kGxShift);
     const uint32_t ki = g_lo(kd);
     kd = kd - kGxShift;
@@ -351,7 +361,8 @@ struct GlibcK {
 // exp(x) for x in [-37.51, 0] or NaN: g_exp without the |x| < 2^-54 case, which the
 // main path already rounds to exactly 1.0 + x there (= 1.0; tests/native pin it), and
 // with the scale taken by ldexp (exact for these normal results).
-__host__ __device__ __forceinline__ double g_exp_neg(double x, const GlibcTables &T, const GlibcK &K = GlibcK()) {
+template <class TT>
+__host__ __device__ __forceinline__ double g_exp_neg(double x, const TT &T, const GlibcK &K = GlibcK()) {
     double kd = __builtin_fma(x, kGxInvLn2N, K.shift);
     const uint32_t ki = g_lo(kd);
     kd = kd - kGxShift;
@@ -407,7 +418,8 @@ __host__ __device__ __forceinline__ double g_log_near1(double x, const GlibcK &K
 }
 // (k folded into the lk / lc tables, see GlibcTables: valid for x in [1 + 0x1.09p-4, 2]
 // and NaN, the box-plus domain of this path)
-__host__ __device__ __forceinline__ double g_log_table(double x, uint32_t hx, const GlibcTables &T,
+template <class TT>
+__host__ __device__ __forceinline__ double g_log_table(double x, uint32_t hx, const TT &T,
                                                        const GlibcK &K) {
 #ifdef QR_EXPERIMENT_UNIFORM_LOG_IDX  // timing only (wrong results)
     const GlibcLogK &c = T.lk[__builtin_amdgcn_readfirstlane(hx >> 13) & 127u];
@@ -428,7 +440,8 @@ __host__ __device__ __forceinline__ double g_log_table(double x, uint32_t hx, co
     pB = __builtin_fma(pB, r2, pA);
     return __builtin_fma(r3, pB, lo) + hi;
 }
-__host__ __device__ __forceinline__ double g_log_u(double x, const GlibcTables &T, const GlibcK &K = GlibcK()) {
+template <class TT>
+__host__ __device__ __forceinline__ double g_log_u(double x, const TT &T, const GlibcK &K = GlibcK()) {
     const uint32_t hx = g_hi(x);
     if (hx < 0x3FF10900u) return g_log_near1(x, K);  // u in [1, 1 + 0x1.09p-4)
     return g_log_table(x, hx, T, K);
@@ -439,7 +452,8 @@ __host__ __device__ __forceinline__ double g_log_u(double x, const GlibcTables &
 // both chains anyway -- one after the other, each a serial dependency chain whose
 // table path starts with an LDS read.  As one basic block the two chains (and those
 // of the other h of the box-plus) interleave and hide each other's latency.
-__host__ __device__ __forceinline__ double g_log_u_sel(double x, const GlibcTables &T, const GlibcK &K = GlibcK()) {
+template <class TT>
+__host__ __device__ __forceinline__ double g_log_u_sel(double x, const TT &T, const GlibcK &K = GlibcK()) {
     const uint32_t hx = g_hi(x);
     const double yn = g_log_near1(x, K);
     const double yt = g_log_table(x, hx, T, K);
@@ -452,8 +466,8 @@ __host__ __device__ __forceinline__ double g_log_u_sel(double x, const GlibcTabl
 // every t >= 36.74, inf included); NaN fails the compare and propagates.
 // The argument may carry a sign: h(|s|) (the box-plus passes a + b and a - b; the abs
 // and the negation fold into the source modifiers of exp's first fmas).
-template <bool SEL = false>
-__host__ __device__ __forceinline__ double h_strict(double s, const GlibcTables &T, const GlibcK &K = GlibcK()) {
+template <bool SEL = false, class TT = GlibcTables>
+__host__ __device__ __forceinline__ double h_strict(double s, const TT &T, const GlibcK &K = GlibcK()) {
     const double tc = g_make((fabs(s) > 37.5) ? 0x4042C000u : g_hi(s), g_lo(s));
     const double u = 1.0 + g_exp_neg(-fabs(tc), T, K);
     return SEL ? g_log_u_sel(u, T, K) : g_log_u(u, T, K);
@@ -497,8 +511,8 @@ __host__ __device__ __forceinline__ double signed_min(double a, double b) {
 #ifndef QR_STRICT_SEL
 #define QR_STRICT_SEL 0
 #endif
-template <bool SEL>
-__host__ __device__ __forceinline__ double box_plus_strict_t(double a, double b, const GlibcTables &T,
+template <bool SEL, class TT>
+__host__ __device__ __forceinline__ double box_plus_strict_t(double a, double b, const TT &T,
                                                             const GlibcK &K = GlibcK()) {
     const double sm = signed_min(a, b);
 #if QR_STRICT_MAXMIN
@@ -513,7 +527,8 @@ __host__ __device__ __forceinline__ double box_plus_strict_t(double a, double b,
     return (sm + h_strict<SEL>(a + b, T, K)) - h_strict<SEL>(a - b, T, K);
 #endif
 }
-__host__ __device__ __forceinline__ double box_plus_strict(double a, double b, const GlibcTables &T,
+template <class TT>
+__host__ __device__ __forceinline__ double box_plus_strict(double a, double b, const TT &T,
                                                           const GlibcK &K = GlibcK()) {
     return box_plus_strict_t<QR_STRICT_SEL != 0>(a, b, T, K);
 }

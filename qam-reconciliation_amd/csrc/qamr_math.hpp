@@ -224,17 +224,21 @@ QR_HD int search_bracket(const SearchCmp &cmp, double &lo, double &hi) {
 // (quick() is monotone in the probe, so the smaller probes agree with 2^(m*-1)); any probe
 // inside the window, or a rounding that breaks the verification, takes the loop.  Same
 // lo, hi and guard as the loop, ~20 instructions instead of ~20 per doubling.
+// Off by default (QR_BRACKET_FAST=0): it is exact (host replay check) but its extra live values
+// cost the hypothesis-parallel demapper an occupancy step (130 VGPRs -> 3 waves/SIMD).
+#ifndef QR_BRACKET_FAST
+#define QR_BRACKET_FAST 0
+#endif
 QR_HD int search_bracket_fast(const SearchCmp &cmp, double &lo, double &hi) {
-    if (!cmp.have) return search_bracket(cmp, lo, hi);
     const bool up = cmp.T > .5;
     const double z = up ? cmp.ystar : -cmp.ystar;
     const double x = z + cmp.W;
     const int m = (x < 1.0) ? 0 : ilogb(x) + 1;
-    if (!(m >= 0 && m <= 1000)) return search_bracket(cmp, lo, hi);
     const double p = ldexp(1.0, m), q = (m > 0) ? ldexp(1.0, m - 1) : 0.0;
-    const double stop = up ? p : -p, prev = up ? q : -q;
     const int want = up ? 1 : -1;   // the stopping probe: F(2^m) > T (up) / F(-2^m) < T (down)
-    if (cmp.quick(stop) != want || (m > 0 && cmp.quick(prev) != -want)) return search_bracket(cmp, lo, hi);
+    const bool ok = cmp.have && m >= 0 && m <= 1000 && cmp.quick(up ? p : -p) == want &&
+                    (m == 0 || cmp.quick(up ? q : -q) == -want);
+    if (!ok) return search_bracket(cmp, lo, hi);   // the one fallback (window probes, rounding)
     lo = up ? q : -p;
     hi = up ? p : -q;
     return m;
@@ -269,7 +273,7 @@ QR_HD double search_replay(const SearchCmp &cmp) {
 // search_closed_finish applies the exact answer gt = (F_Y(end) > T).
 QR_HD bool search_closed_prepare(const SearchCmp &cmp, double &L, double &H, int &need) {
     double lo, hi;
-    const int guard = search_bracket_fast(cmp, lo, hi);
+    const int guard = QR_BRACKET_FAST ? search_bracket_fast(cmp, lo, hi) : search_bracket(cmp, lo, hi);
     const double width = hi - lo;
     need = 0;
     if (!(width > 1e-9) || !(width <= 0x1p20) || !(cmp.W < 0x1p-31)) return false;

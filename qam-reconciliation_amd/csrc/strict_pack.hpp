@@ -58,8 +58,8 @@ __host__ __device__ constexpr int pack_out_round(int D, int i) {
 // and for every t > 37.5 exp(-t) < 2^-54, so u = fl(1.0 + exp(-t)) == 1.0 and h == +0 in all
 // three modes: the same bits.
 enum { kClampNone = 0, kClampFull = 1, kClampFinite = 2 };
-template <int CL = kClampFull, int MJ = kPackMaxJobs>
-__device__ __forceinline__ void h_packed(const double *t, double *h, int nj, double *wb, const GlibcTables &T,
+template <int CL = kClampFull, int MJ = kPackMaxJobs, class TT = GlibcTables>
+__device__ __forceinline__ void h_packed(const double *t, double *h, int nj, double *wb, const TT &T,
                                          const GlibcK &K) {
     constexpr int kPackMaxJobs = MJ;  // (shadows the namespace constant: MJ arguments per lane)
     constexpr int S = 64 * MJ + 64;
@@ -142,9 +142,9 @@ __device__ __forceinline__ double signed_min_packed(double a, double b) {
 // as check_exact<kStrict>, evaluated round by round.
 // NC checks of degree D side by side (the same rounds; their log arguments packed together:
 // one partly filled slice per kind and round for all NC checks instead of one per check).
-template <int D, int CL = kClampFull, int NC = 1>
+template <int D, int CL = kClampFull, int NC = 1, class TT = GlibcTables>
 __device__ __forceinline__ void check_strict_packed_n(const double (&m)[NC][D], double (&out)[NC][D], double *wb,
-                                                      const GlibcTables &T, const GlibcK &K) {
+                                                      const TT &T, const GlibcK &K) {
     if constexpr (D == 2) {
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
@@ -202,9 +202,9 @@ __device__ __forceinline__ void check_strict_packed_n(const double (&m)[NC][D], 
         }
     }
 }
-template <int D, int CL = kClampFull>
+template <int D, int CL = kClampFull, class TT = GlibcTables>
 __device__ __forceinline__ void check_strict_packed(const double (&m)[D], double (&out)[D], double *wb,
-                                                    const GlibcTables &T, const GlibcK &K) {
+                                                    const TT &T, const GlibcK &K) {
     check_strict_packed_n<D, CL, 1>(reinterpret_cast<const double(&)[1][D]>(m), reinterpret_cast<double(&)[1][D]>(out),
                                     wb, T, K);
 }
