@@ -217,6 +217,12 @@ __device__ __forceinline__ void stage_tables(typename Arith<AR>::Tab *lds, const
 #ifndef QR_CHECK_GLDS
 #define QR_CHECK_GLDS 0
 #endif
+#ifndef QR_LOAD_BEFORE_STORE
+#define QR_LOAD_BEFORE_STORE 0
+#endif
+#ifndef QR_STORE_RECOMPUTE
+#define QR_STORE_RECOMPUTE 0
+#endif
 template <int D, int MODE, bool NT>
 struct CheckIn {
     double p[D], c[D];
@@ -317,10 +323,16 @@ struct PackLds {
     static constexpr int doubles = (AR == kStrict && QR_STRICT_PACK) ? 4 * kPackWaveStride : 1;
 };
 
-template <int AR, int D, bool NT, bool FIN = false>
+struct NoPre {
+    __device__ __forceinline__ void operator()() const {}
+};
+// pre(): called in the packed path after the outputs are computed and before they are stored
+// (QR_LOAD_BEFORE_STORE: the next check's loads are issued ahead of this check's stores, so the
+// wait for them does not include the stores' completion -- gfx9 counts both in vmcnt).
+template <int AR, int D, bool NT, bool FIN = false, class Pre = NoPre>
 __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m)[D], int base, uint8_t sb, uint32_t b8,
                                             const typename Arith<AR>::Tab &tab, const typename Arith<AR>::Regs &K,
-                                            double *hb = nullptr, bool live = true) {
+                                            double *hb = nullptr, bool live = true, Pre pre = Pre{}) {
     const int ld = a.ld;
     const double s = sb ? -1.0 : 1.0;
     if constexpr (AR == kStrict && QR_STRICT_PACK && D <= kPackMaxDeg) {
@@ -343,9 +355,17 @@ __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m
         } else {
             check_strict_packed<D, kClampFull>(m, out, wb, tab, K);
         }
+        pre();
 #pragma unroll
-        for (int i = 0; i < D; ++i)
-            if (live) st_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), ld), b8, ld, s * out[i]);
+        for (int i = 0; i < D; ++i) {
+            int e = sld(a.chk_edge + base + i);
+#if QR_STORE_RECOMPUTE
+            // a fresh value for the compiler: the store's row pointer and buffer resource are
+            // rebuilt here (a few SALU) instead of held in SGPRs across the whole update
+            asm volatile("" : "+s"(e));
+#endif
+            if (live) st_row<NT>(row_ptr(a.c2v, e, ld), b8, ld, s * out[i]);
+        }
         return;
     }
     double F[D - 1];
@@ -438,6 +458,10 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
         if (MODE != kFirst && bad && act && live) a.unsat[f] = 1;
         return;
     }
+    // the next check's loads issued between this check's arithmetic and its stores (packed
+    // strict update only: its outputs are all in registers at that point)
+    constexpr bool kLoadBeforeStore = QR_LOAD_BEFORE_STORE && !kPrefetch && !GL && MODE != kParityOnly &&
+                                      AR == kStrict && QR_STRICT_PACK && D <= kPackMaxDeg;
     CheckIn<D, MODE, NT> nx;
     uint32_t *pg = GL ? pgb + (threadIdx.x >> 6) * (D * 128) : nullptr;
     if constexpr (GL) nx.load_glds(a, ci, f, pg);
@@ -479,12 +503,16 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
                 } else {
                     check_exact<kFast, D, NT>(a, m, cur.base, cur.sb, b8, tab, Arith<kFast>::Regs{}, nullptr, live);
                 }
+            } else if constexpr (kLoadBeforeStore) {
+                check_exact<AR, D, NT, FIN>(a, m, cur.base, cur.sb, b8, tab, K, hb, live, [&]() {
+                    if (more) nx.load(a, cn, f);
+                });
             } else {
                 check_exact<AR, D, NT, FIN>(a, m, cur.base, cur.sb, b8, tab, K, hb, live);
             }
         }
         if (!more) break;
-        if (!kPrefetch && !GL) nx.load(a, cn, f);
+        if (!kPrefetch && !GL && !kLoadBeforeStore) nx.load(a, cn, f);
         ci = cn;
     }
     if (MODE != kFirst && bad && act && live) a.unsat[f] = 1;  // benign race: every writer stores 1
