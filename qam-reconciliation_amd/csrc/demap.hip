@@ -169,12 +169,23 @@ k_demap_hyp(const DemapTables *__restrict__ tab,
 #pragma unroll 1
         for (int h = 0; h < HPW; ++h) {
             const int i = w + h * W;
+#if defined(QR_EXPERIMENT_NO_SEARCH)   // cost breakdown only (wrong results): the start point
+            const double y = quantile_start(t, i, search_target(t, nv, i));
+#elif defined(QR_EXPERIMENT_NEWTON_ONLY)   // cost breakdown only: start + Newton, no bracket/bisection
+            double y = 0, Wd = 0;
+            newton_root(t, *gmt, search_target(t, nv, i), i, y, Wd);
+#else
             const double y = g_inv_search_wave<M>(t, *gmt, nv, i, ey[w], et[w], lane);
+#endif
             // noisemapper.pyx:503-515 in the reference's summation order (k < j, p[j], k > j)
             // as one loop with the argument selected per lane (see demap_symbol)
             double sum = 0;
 #pragma unroll QR_DEMAP_HYP_UNROLL
             for (int k = 0; k < M; ++k) {
+#ifdef QR_EXPERIMENT_NO_LLR   // cost breakdown only (wrong results)
+                sum += y * t.p[k];
+                continue;
+#endif
                 const double e = (2 * y - t.a[k] - aj) * (t.a[k] - aj);
                 // (k == j: the term is p[j]; its exp argument, 0, would send the wave down the
                 // special-case path of g_exp_wave for nothing)
