@@ -806,16 +806,27 @@ static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
 // Runtime tuning knobs (qr_tune_set); defaults picked by scripts/tune.py on MI355X.
 struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3}, math{kStrict}, eps_max{40},
-        lds_pad_kb{0}, compact{1}, side{1};
+        lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048};
 };
 static Tuning g_tune;
 
-static Geom make_geom(int ncols, int ft_req, int per) {
+// Frame tile ft (a divisor of ncols, <= ft_req) and nodes per thread.  Small problems (few
+// nodes x few frame tiles, e.g. the reg-(3,6) N=1008 code of configs[1]) get fewer nodes per
+// thread, down to 1, so that a launch still has ~min_blocks workgroups to spread over the
+// 256 CUs (knob min_blocks, 0 = off); the DVB-S2 launches keep their per.
+static Geom make_geom(int ncols, int ft_req, int per, int64_t nodes = 0) {
     int ft = 256;
     while (ft > 64 && (ft > ft_req || ncols % ft)) ft >>= 1;
     int lft = 6;
     while ((1 << lft) < ft) ++lft;
-    return Geom{lft, per < 1 ? 1 : per};
+    per = per < 1 ? 1 : per;
+    const int64_t target = g_tune.min_blocks.load();
+    if (nodes > 0 && target > 0) {
+        const int64_t tiles = ncols >> lft, nsub = 256 >> lft;
+        const int64_t fit = nodes * tiles / (target * nsub);   // per that gives ~target blocks
+        if (fit < per) per = (int)(fit < 1 ? 1 : fit);
+    }
+    return Geom{lft, per};
 }
 
 // Everything one decode call needs to issue its launches.
@@ -849,7 +860,7 @@ struct Plan {
         a.unsat = unsat;
         a.ld = ld;
         a.f_off = f0;
-        a.g = make_geom(f1 - f0, g_tune.check_ft.load(), g_tune.check_per.load());
+        a.g = make_geom(f1 - f0, g_tune.check_ft.load(), g_tune.check_per.load(), cls.n);
         const int64_t per_block = (int64_t)a.g.per * (256 >> a.g.lft);
         a.nbx = (unsigned)((cls.n + per_block - 1) / per_block);
         a.gtab = code->d_mtab;
@@ -872,7 +883,7 @@ struct Plan {
         a.active = w.active;
         a.ld = ld;
         a.f_off = f0;
-        a.g = make_geom(f1 - f0, g_tune.var_ft.load(), g_tune.var_per.load());
+        a.g = make_geom(f1 - f0, g_tune.var_ft.load(), g_tune.var_per.load(), code->V);
         const int64_t per_block = (int64_t)a.g.per * (256 >> a.g.lft);
         a.nbx = (unsigned)((code->V + per_block - 1) / per_block);
         a.alist = a.acount = nullptr;
@@ -1444,7 +1455,7 @@ int qr_tune_set(const char *name, int64_t value) {
                         : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
                         : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
                         : n == "math"     ? &g_tune.math     : n == "lds_pad_kb" ? &g_tune.lds_pad_kb : n == "eps_max"   ? &g_tune.eps_max
-                        : n == "compact" ? &g_tune.compact : n == "side" ? &g_tune.side : n == "demap_fast" ? &g_demap_fast : n == "demap_hyp" ? &g_demap_hyp : nullptr;
+                        : n == "compact" ? &g_tune.compact : n == "side" ? &g_tune.side : n == "demap_fast" ? &g_demap_fast : n == "demap_hyp" ? &g_demap_hyp : n == "min_blocks" ? &g_tune.min_blocks : nullptr;
     if (!k) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     if (value < 0 || value > 4096) return set_error(QR_EVALUE, "tuning value out of range");
     k->store((int)value);
@@ -1457,7 +1468,7 @@ int qr_tune_get(const char *name, int64_t *value) {
                               : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
                               : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
                               : n == "math"     ? &g_tune.math     : n == "lds_pad_kb" ? &g_tune.lds_pad_kb : n == "eps_max"   ? &g_tune.eps_max
-                              : n == "compact" ? &g_tune.compact : n == "side" ? &g_tune.side : n == "demap_fast" ? &g_demap_fast : n == "demap_hyp" ? &g_demap_hyp : nullptr;
+                              : n == "compact" ? &g_tune.compact : n == "side" ? &g_tune.side : n == "demap_fast" ? &g_demap_fast : n == "demap_hyp" ? &g_demap_hyp : n == "min_blocks" ? &g_tune.min_blocks : nullptr;
     if (!k || !value) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     *value = k->load();
     return QR_OK;
