@@ -806,7 +806,7 @@ static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
 // Runtime tuning knobs (qr_tune_set); defaults picked by scripts/tune.py on MI355X.
 struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3}, math{kStrict}, eps_max{40},
-        lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048};
+        lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024};
 };
 static Tuning g_tune;
 
@@ -1269,9 +1269,18 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     // decoder.pyx:408-421: c2v = 0, first variable sweep.
     if ((rc = launch_var<true>(P, 0, ld))) return rc;
     int max_deg = 0;
-    for (const auto &c : code->classes) max_deg = std::max(max_deg, c.degree);
+    int64_t max_n = 0;
+    for (const auto &c : code->classes) max_deg = std::max(max_deg, c.degree), max_n = std::max(max_n, c.n);
     const int sp = g_tune.split.load();
-    const bool split = sp >= 2 && ld % 512 == 0 && max_deg <= 16;
+    // The split schedules overlap one half's check sweep with the other half's variable sweep;
+    // that pays only when a half's check launch fills the chip on its own (DVB-S2 N=64800:
+    // 1013 check blocks x 16 frame tiles at B = 4096).  A small code (configs[1]: reg-(3,6)
+    // N=1008, B = 1024: 64 blocks) runs all frames in lock-step instead -- 4.9x the frames/s
+    // of the split schedule on MI355X.  Knob split_min_blocks (0 = always split).
+    const Geom gh = make_geom(ld / 2, g_tune.check_ft.load(), g_tune.check_per.load());
+    const int64_t half_blocks = (max_n + (int64_t)gh.per * (256 >> gh.lft) - 1) / ((int64_t)gh.per * (256 >> gh.lft)) *
+                                ((ld / 2) >> gh.lft);
+    const bool split = sp >= 2 && ld % 512 == 0 && max_deg <= 16 && half_blocks >= g_tune.split_min_blocks.load();
     // active-frame lists of the ranges the schedule sweeps (after the iteration-0 status)
     P.compact = g_tune.compact.load() != 0;
     if (split) {
@@ -1455,7 +1464,7 @@ int qr_tune_set(const char *name, int64_t value) {
                         : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
                         : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
                         : n == "math"     ? &g_tune.math     : n == "lds_pad_kb" ? &g_tune.lds_pad_kb : n == "eps_max"   ? &g_tune.eps_max
-                        : n == "compact" ? &g_tune.compact : n == "side" ? &g_tune.side : n == "demap_fast" ? &g_demap_fast : n == "demap_hyp" ? &g_demap_hyp : n == "min_blocks" ? &g_tune.min_blocks : nullptr;
+                        : n == "compact" ? &g_tune.compact : n == "side" ? &g_tune.side : n == "demap_fast" ? &g_demap_fast : n == "demap_hyp" ? &g_demap_hyp : n == "min_blocks" ? &g_tune.min_blocks : n == "split_min_blocks" ? &g_tune.split_min_blocks : nullptr;
     if (!k) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     if (value < 0 || value > 4096) return set_error(QR_EVALUE, "tuning value out of range");
     k->store((int)value);
@@ -1468,7 +1477,7 @@ int qr_tune_get(const char *name, int64_t *value) {
                               : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
                               : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
                               : n == "math"     ? &g_tune.math     : n == "lds_pad_kb" ? &g_tune.lds_pad_kb : n == "eps_max"   ? &g_tune.eps_max
-                              : n == "compact" ? &g_tune.compact : n == "side" ? &g_tune.side : n == "demap_fast" ? &g_demap_fast : n == "demap_hyp" ? &g_demap_hyp : n == "min_blocks" ? &g_tune.min_blocks : nullptr;
+                              : n == "compact" ? &g_tune.compact : n == "side" ? &g_tune.side : n == "demap_fast" ? &g_demap_fast : n == "demap_hyp" ? &g_demap_hyp : n == "min_blocks" ? &g_tune.min_blocks : n == "split_min_blocks" ? &g_tune.split_min_blocks : nullptr;
     if (!k || !value) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
     *value = k->load();
     return QR_OK;
