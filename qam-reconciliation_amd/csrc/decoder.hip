@@ -170,6 +170,8 @@ struct VarArgs {
     Geom g;
     unsigned nbx;
     const int32_t *alist, *acount;  // as CheckArgs
+    unsigned nby;  // frame tiles (grid-stride launches)
+    int gs;        // 1: a capped 1-D grid walks the nbx x nby tiles (the paced sweeps of run_split2, knob var_pace)
 };
 
 // Active-frame compaction (converging operating points, decoder.pyx:431-433: frames stop
@@ -550,6 +552,34 @@ __device__ __forceinline__ void var_block(const VarArgs &a, unsigned bx, unsigne
 #ifndef QR_CHECK_STRICT_WAVES
 #define QR_CHECK_STRICT_WAVES 1
 #endif
+// QR_EXPERIMENT_CLOCK (diagnostic builds only, scripts/diag/clock_check.py): every workgroup of
+// the degree-7 main-loop check sweep stamps the shader clock (s_memtime) and the 100 MHz
+// realtime counter around its work and adds both spans to g_clk (vector atomics); the effective
+// clock of the unprofiled launch is sum(cycles) / sum(ticks) x 100 MHz (MI355X_MICROARCH.md
+// 'DVFS give-back' item 6).  qr_debug_clock reads and clears the sums.
+#ifndef QR_EXPERIMENT_CLOCK
+#define QR_EXPERIMENT_CLOCK 0
+#endif
+#if QR_EXPERIMENT_CLOCK
+__device__ unsigned long long g_clk[3];
+struct ClkScope {
+    bool on;
+    uint64_t c0, r0;
+    __device__ explicit ClkScope(bool on_) : on(on_) {
+        c0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    __device__ ~ClkScope() {
+        __syncthreads();
+        if (on && threadIdx.x == 0) {
+            const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+            atomicAdd(&g_clk[0], (unsigned long long)(c1 - c0));
+            atomicAdd(&g_clk[1], (unsigned long long)(r1 - r0));
+            atomicAdd(&g_clk[2], 1ull);
+        }
+    }
+};
+#endif
 template <int D, int MODE, bool NT, int AR>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AR == kStrict ? QR_CHECK_STRICT_WAVES : 1, 8)))
 k_check(CheckArgs a) {
@@ -558,6 +588,9 @@ k_check(CheckArgs a) {
     __shared__ double hb[PackLds<AR>::doubles];
     __shared__ uint32_t pgb[GL ? 4 * D * 128 : 1];   // 4 waves x D posterior rows (LDS DMA)
     if (!frames_block_live(a.acount, blockIdx.y, a.g.lft)) return;  // block-uniform
+#if QR_EXPERIMENT_CLOCK
+    ClkScope clk(D == 7 && MODE == kNormal && AR == kStrict);
+#endif
     if (MODE != kParityOnly) stage_tables<AR>(&tab, a);
     if constexpr (AR == kStrict && MODE != kParityOnly && QR_STRICT_FINITE && QR_STRICT_PACK && D <= kPackMaxDeg) {
         if (a.finite && sld(a.finite)) {  // kernel-uniform: one of the two bodies runs
@@ -581,6 +614,14 @@ __global__ void __launch_bounds__(256) k_finite(const double *__restrict__ lappr
 
 template <bool INIT, bool NT>
 __global__ void __launch_bounds__(256) k_var(VarArgs a) {
+    if (a.gs) {  // capped grid: tile t = (bx fastest, by), the grid's blocks sweep a moving window
+        const unsigned n = a.nbx * a.nby;
+        for (unsigned t = blockIdx.x; t < n; t += gridDim.x) {
+            const unsigned by = t / a.nbx, bx = t - by * a.nbx;
+            if (frames_block_live(a.acount, by, a.g.lft)) var_block<INIT, NT>(a, bx, by);
+        }
+        return;
+    }
     if (!frames_block_live(a.acount, blockIdx.y, a.g.lft)) return;
     var_block<INIT, NT>(a, blockIdx.x, blockIdx.y);
 }
@@ -806,7 +847,7 @@ static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
 // Runtime tuning knobs (qr_tune_set); defaults picked by scripts/tune.py on MI355X.
 struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3}, math{kStrict}, eps_max{40},
-        lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024};
+        lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024}, var_pace{28};
 };
 static Tuning g_tune;
 
@@ -843,6 +884,7 @@ struct Plan {
     hipStream_t s;
     int lds_pad = 0;  // dynamic LDS reserved by each check workgroup (caps their CU residency)
     bool compact = false;  // sweeps of the main loop read the active-frame lists
+    int var_pace = 0;      // variable sweeps: workgroups per frame tile (0 = one per tile)
 
     const int32_t *count_of(int f0) const { return w.acount + (f0 == 0 ? 0 : 1); }
 
@@ -887,6 +929,8 @@ struct Plan {
         const int64_t per_block = (int64_t)a.g.per * (256 >> a.g.lft);
         a.nbx = (unsigned)((code->V + per_block - 1) / per_block);
         a.alist = a.acount = nullptr;
+        a.nby = (unsigned)((f1 - f0) >> a.g.lft);
+        a.gs = 0;
         return a;
     }
 };
@@ -957,7 +1001,16 @@ static int launch_var(const Plan &P, int f0, int f1) {
         a.alist = P.w.alist;
         a.acount = P.count_of(f0);
     }
-    dim3 grid(a.nbx, (unsigned)((f1 - f0) >> a.g.lft));
+    dim3 grid(a.nbx, a.nby);
+    // Paced sweep (the two-stream schedule's variable sweeps, Plan::var_pace): at most var_pace
+    // workgroups per frame tile, each walking tiles grid-stride, so that the sweep streams its
+    // bytes over about the length of the concurrent check sweep instead of saturating HBM for
+    // the first ~40 % of it.
+    const int64_t cap = (int64_t)P.var_pace * a.nby;
+    if (cap > 0 && (int64_t)a.nbx * a.nby > cap) {
+        a.gs = 1;
+        grid = dim3((unsigned)cap, 1);
+    }
     if (P.nt) k_var<INIT, true><<<grid, 256, 0, P.s>>>(a);
     else k_var<INIT, false><<<grid, 256, 0, P.s>>>(a);
     QR_LAUNCH_CHECK();
@@ -1100,13 +1153,17 @@ static int run_split(const Plan &P, int max_it) {
 // The variable sweep's 12-VGPR waves fill whatever the 128-VGPR check waves leave of
 // each SIMD and stream their messages under the check sweep's fp64 arithmetic (in
 // the fused launch they take whole check-sized slots instead): 5.15 vs 5.35 ms per
-// half-iteration for the strict arithmetic (MI355X, B=4096).  Knob lds_pad_kb reserves
+// half-iteration for the strict arithmetic (MI355X, B=4096).  The variable sweeps are paced
+// (knob var_pace, workgroups per frame tile, default 28): unpaced, the sweep saturates HBM for
+// the first ~1.7 ms of the 4.3 ms check launch beside it and the check sweep's gathers stall
+// (VALU issue 0.72 of the launch); paced to stream over the whole check launch, 4.15 ms and
+// 0.85 (MI355X, B=4096: 8.96 k -> 9.70 k frames/s on one box).  Knob lds_pad_kb reserves
 // LDS per check workgroup to cap their residency (40/48 KB -> 3 per CU: 5.22-5.26 ms;
 // 64 KB -> 2: 5.65 ms; 0 = default).
-static int run_split2(const Plan &P, int max_it) {
-    const qr_code *code = P.code;
-    std::lock_guard<std::mutex> lk(code->mu);
-    if (!code->s2) {  // first use: all or nothing
+// The second stream of the two-stream schedules and its events, created on first use (all or
+// nothing; the caller holds code->mu).
+static int side_stream(const qr_code *code, hipStream_t *out) {
+    if (!code->s2) {
         hipStream_t s2 = nullptr;
         hipEvent_t ev[5] = {};
         hipError_t e = hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
@@ -1120,9 +1177,19 @@ static int run_split2(const Plan &P, int max_it) {
         for (int i = 0; i < 5; ++i) code->ev[i] = ev[i];
         code->s2 = s2;
     }
+    *out = code->s2;
+    return QR_OK;
+}
+
+static int run_split2(const Plan &P, int max_it) {
+    const qr_code *code = P.code;
+    std::lock_guard<std::mutex> lk(code->mu);
+    hipStream_t s2 = nullptr;
+    if (int rc0 = side_stream(code, &s2)) return rc0;
     hipEvent_t fork = code->ev[0], cA = code->ev[1], cB = code->ev[2], vA = code->ev[3], vB = code->ev[4];
     Plan V = P;
-    V.s = code->s2;
+    V.s = s2;
+    V.var_pace = g_tune.var_pace.load();
     Plan C = P;
     C.lds_pad = std::max(0, g_tune.lds_pad_kb.load()) * 1024;
     const int ld = P.ld, h = ld / 2;
@@ -1192,25 +1259,13 @@ static int run_split2(const Plan &P, int max_it) {
 static int run_pipes(const Plan &P, int max_it) {
     const qr_code *code = P.code;
     std::lock_guard<std::mutex> lk(code->mu);
-    if (!code->s2) {  // first use: all or nothing
-        hipStream_t s2 = nullptr;
-        hipEvent_t ev[5] = {};
-        hipError_t e = hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
-        for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
-        if (e != hipSuccess) {
-            for (auto x : ev)
-                if (x) (void)hipEventDestroy(x);
-            if (s2) (void)hipStreamDestroy(s2);
-            return set_error(QR_EDEVICE, "decode: second stream: %s", hipGetErrorString(e));
-        }
-        for (int i = 0; i < 5; ++i) code->ev[i] = ev[i];
-        code->s2 = s2;
-    }
+    hipStream_t s2 = nullptr;
+    if (int rc0 = side_stream(code, &s2)) return rc0;
     hipEvent_t fork = code->ev[0], join = code->ev[4];
     const int ld = P.ld, h = ld / 2;
     auto row = [&](int t) { return P.w.unsat + (size_t)t * ld; };
     Plan PB = P;
-    PB.s = code->s2;
+    PB.s = s2;
     QR_HIP(hipEventRecord(fork, P.s));
     QR_HIP(hipStreamWaitEvent(PB.s, fork, 0));
     int rc;
@@ -1458,27 +1513,48 @@ int qr_code_create(const int64_t *e_to_v, const int64_t *e_to_c, int64_t nv, int
 
 int qr_code_destroy(qr_code *code) { return free_code(code); }
 
-int qr_tune_set(const char *name, int64_t value) {
+#if QR_EXPERIMENT_CLOCK
+// Diagnostic builds only (not in include/qamr.h): out = {sum cycles, sum ticks, workgroups}.
+QR_API int qr_debug_clock(int64_t *out) {
+    unsigned long long h[3] = {0, 0, 0};
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(qr::g_clk), sizeof(h)) != hipSuccess) return QR_EDEVICE;
+    const unsigned long long z[3] = {0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(qr::g_clk), z, sizeof(z)) != hipSuccess) return QR_EDEVICE;
+    for (int i = 0; i < 3; ++i) out[i] = (int64_t)h[i];
+    return QR_OK;
+}
+#endif
+
+// name -> knob (nullptr if unknown)
+static std::atomic<int> *tune_knob(const char *name) {
+    static const std::pair<const char *, std::atomic<int> *> knobs[] = {
+        {"check_ft", &g_tune.check_ft},     {"check_per", &g_tune.check_per},
+        {"var_ft", &g_tune.var_ft},         {"var_per", &g_tune.var_per},
+        {"nt", &g_tune.nt},                 {"split", &g_tune.split},
+        {"math", &g_tune.math},             {"lds_pad_kb", &g_tune.lds_pad_kb},
+        {"eps_max", &g_tune.eps_max},       {"compact", &g_tune.compact},
+        {"side", &g_tune.side},             {"demap_fast", &g_demap_fast},
+        {"demap_hyp", &g_demap_hyp},        {"min_blocks", &g_tune.min_blocks},
+        {"split_min_blocks", &g_tune.split_min_blocks},
+        {"var_pace", &g_tune.var_pace},
+    };
     const std::string n = name ? name : "";
-    std::atomic<int> *k = n == "check_ft" ? &g_tune.check_ft : n == "check_per" ? &g_tune.check_per
-                        : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
-                        : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
-                        : n == "math"     ? &g_tune.math     : n == "lds_pad_kb" ? &g_tune.lds_pad_kb : n == "eps_max"   ? &g_tune.eps_max
-                        : n == "compact" ? &g_tune.compact : n == "side" ? &g_tune.side : n == "demap_fast" ? &g_demap_fast : n == "demap_hyp" ? &g_demap_hyp : n == "min_blocks" ? &g_tune.min_blocks : n == "split_min_blocks" ? &g_tune.split_min_blocks : nullptr;
-    if (!k) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
+    for (const auto &k : knobs)
+        if (n == k.first) return k.second;
+    return nullptr;
+}
+
+int qr_tune_set(const char *name, int64_t value) {
+    std::atomic<int> *k = tune_knob(name);
+    if (!k) return set_error(QR_EVALUE, "unknown tuning knob '%s'", name ? name : "");
     if (value < 0 || value > 4096) return set_error(QR_EVALUE, "tuning value out of range");
     k->store((int)value);
     return QR_OK;
 }
 
 int qr_tune_get(const char *name, int64_t *value) {
-    const std::string n = name ? name : "";
-    const std::atomic<int> *k = n == "check_ft" ? &g_tune.check_ft : n == "check_per" ? &g_tune.check_per
-                              : n == "var_ft"   ? &g_tune.var_ft   : n == "var_per"   ? &g_tune.var_per
-                              : n == "nt"       ? &g_tune.nt       : n == "split"     ? &g_tune.split
-                              : n == "math"     ? &g_tune.math     : n == "lds_pad_kb" ? &g_tune.lds_pad_kb : n == "eps_max"   ? &g_tune.eps_max
-                              : n == "compact" ? &g_tune.compact : n == "side" ? &g_tune.side : n == "demap_fast" ? &g_demap_fast : n == "demap_hyp" ? &g_demap_hyp : n == "min_blocks" ? &g_tune.min_blocks : n == "split_min_blocks" ? &g_tune.split_min_blocks : nullptr;
-    if (!k || !value) return set_error(QR_EVALUE, "unknown tuning knob '%s'", n.c_str());
+    const std::atomic<int> *k = tune_knob(name);
+    if (!k || !value) return set_error(QR_EVALUE, "unknown tuning knob '%s'", name ? name : "");
     *value = k->load();
     return QR_OK;
 }

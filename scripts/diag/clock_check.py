@@ -1,0 +1,74 @@
+"""Diagnostic (MI355X): the shader clock the chip holds DURING the degree-7 check sweep,
+unprofiled, from the in-kernel stamps of a QR_EXPERIMENT_CLOCK build (decoder.hip: every
+workgroup adds its s_memtime / s_memrealtime spans to g_clk), beside the launch time from
+hipEvents, for the default two-stream schedule and any QAMR_TUNE-style variants.
+
+  scripts/exp_build.sh clk "-DQR_EXPERIMENT_CLOCK=1"
+  QAMR_LIB=qam-reconciliation_amd/qamr/exp/libqamr_clk.so python scripts/diag/clock_check.py "" "split=1"
+
+Per variant: step ms, check_d7 launch us (events), effective clock GHz, and the VALU issue
+fraction at that clock (1.585e9 wave-instructions x 4 cycles / 1024 SIMDs per 2048-frame
+launch, scaled by the launch's frames)."""
+import ctypes as C
+import os
+import sys
+import time
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "qam-reconciliation_amd"))
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from qamr import _lib  # noqa: E402
+
+VALU_PER_FRAME = 1.585e9 / 2048  # wave-instructions of one check_d7 launch per frame (PMC, r03)
+
+
+def run(variant, w, L, steps=4):
+    for item in filter(None, variant.split(",")):
+        k, v = item.split("=")
+        _lib.tune_set(k.strip(), int(v))
+    w.step_eager()
+    w.sync()
+    out = (C.c_int64 * 3)()
+    L.qr_debug_clock(out)  # clear
+    _lib.profile_enable(True)
+    _lib.profile_select("check_d7")
+    _lib.profile_reset()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        w.step_eager()
+    w.sync()
+    dt = (time.perf_counter() - t0) / steps
+    ms, n = _lib.profile_query("check_d7")
+    L.qr_debug_clock(out)
+    _lib.profile_enable(False)
+    cyc, ticks, blocks = out[0], out[1], out[2]
+    ghz = cyc / ticks * 0.1 if ticks else float("nan")
+    launch_us = ms / max(n, 1) * 1e3
+    frames = w.B if _lib.tune_get("split") < 2 else w.B // 2
+    issue_us = VALU_PER_FRAME * frames * 4 / 1024 / (ghz * 1e3)
+    print(f"variant '{variant or 'default'}': step {dt * 1e3:.1f} ms, {w.B / dt:.0f} frames/s, check_d7 "
+          f"{launch_us:.0f} us x {n}, clock {ghz:.3f} GHz ({blocks} workgroups), VALU issue {issue_us:.0f} us "
+          f"= {issue_us / launch_us:.3f} of the launch", flush=True)
+
+
+def main():
+    L = _lib.load()
+    L.qr_debug_clock.argtypes = [C.c_void_p]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    w = bench.Work("dvbs2_4pam", None, 4096, 50, 1.0, 0, 0, 0)
+    w.step_eager()
+    w.sync()
+    defaults = {k: _lib.tune_get(k) for k in ("split", "check_per", "check_ft", "var_pace", "var_per")}
+    for variant in sys.argv[1:] or [""]:
+        for k, v in defaults.items():
+            _lib.tune_set(k, v)
+        run(variant, w, L)
+
+
+if __name__ == "__main__":
+    main()
