@@ -307,6 +307,27 @@ def probe_clock(w, n=16, ms=3.0):
         return None
 
 
+def kernel_clock(args):
+    """The shader clock the chip holds DURING the priced check launches, unprofiled: a child
+    process runs the same workload for a few steps on libqamr_clock.so, the diagnostic twin of
+    libqamr.so whose degree-7 check sweep stamps s_memtime / s_memrealtime around every
+    workgroup (decoder.hip QR_EXPERIMENT_CLOCK; MI355X_MICROARCH.md 'DVFS give-back' item 6).
+    Returns its JSON {"clock_ghz", "launch_us", "workgroups", "steps"} or None."""
+    import subprocess
+
+    lib = os.path.join(ROOT, "qam-reconciliation_amd", "qamr", "libqamr_clock.so")
+    if not os.path.exists(lib):
+        return None
+    cmd = [sys.executable, os.path.join(ROOT, "scripts", "diag", "clock_check.py"), "--json",
+           "--workload", args.workload, "--batch", str(args.batch)]
+    try:
+        r = subprocess.run(cmd, env=dict(os.environ, QAMR_LIB=lib), capture_output=True, text=True, timeout=240)
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        return d if d.get("clock_ghz", 0) > 0 else None
+    except Exception:
+        return None
+
+
 def kernel_stats():
     import qamr
 
@@ -319,7 +340,7 @@ def kernel_stats():
     return out
 
 
-def roofline(args, w, kstats, dev):
+def roofline(args, w, kstats, dev, world=1):
     """The dominant kernel's algorithmic bytes per launch / its average launch time."""
     import qamr
 
@@ -368,13 +389,18 @@ def roofline(args, w, kstats, dev):
                     # every wave64 VALU instruction (fp64 or 32-bit) holds its SIMD for one
                     # quad-cycle in this kernel (SQ_ACTIVE_INST_VALU == SQ_INSTS_VALU)
                     clk_pmc = t.get("clock_ghz_pmc")
-                    clk_live = probe_clock(w)
-                    clk = clk_live or clk_pmc or CLOCK_HZ / 1e9
+                    kc = kernel_clock(args) if (world == 1 and kkey == "check_d7") else None
+                    clk_kernel = kc["clock_ghz"] if kc else None
+                    clk_live = None if clk_kernel else probe_clock(w)
+                    clk = clk_kernel or clk_live or clk_pmc or CLOCK_HZ / 1e9
                     busy = 4 * n_all / SIMDS / (clk * 1e9)  # s of SIMD issue time
                     valu = {"wave_insts_per_launch": int(n_all), "f64_wave_insts_per_launch": int(n64),
                             "clock_ghz": round(clk, 3),
-                            "clock_source": "live (qr_clock_probe beside an unprofiled step)" if clk_live
+                            "clock_source": "in-kernel stamps of the check launches (libqamr_clock.so, "
+                                            "unprofiled, same workload)" if clk_kernel
+                            else "live (qr_clock_probe beside an unprofiled step)" if clk_live
                             else "profiled PMC pass" if clk_pmc else "spec",
+                            "clock_pass": kc,
                             "clock_ghz_probe_min_max": getattr(probe_clock, "spread", None) if clk_live else None,
                             "clock_ghz_pmc": round(clk_pmc, 3) if clk_pmc else None,
                             "issue_ms": round(busy * 1e3, 3),
@@ -383,8 +409,9 @@ def roofline(args, w, kstats, dev):
                             "source": t.get("source"),
                             "note": "SIMD issue time of the launch's VALU instructions (4 cycles per wave64 "
                                     "instruction, counts from profiles/pmc_traffic.json, rocprofv3 --pmc) at the "
-                                    "shader clock read by in-kernel s_memtime/s_memrealtime probes running "
-                                    "beside an unprofiled step, over the live launch time; clock_ghz_pmc = "
+                                    "shader clock the check launches run at (s_memtime / s_memrealtime spans of "
+                                    "their workgroups in an unprofiled pass of the diagnostic twin library), over "
+                                    "the live launch time; clock_ghz_pmc = "
                                     "GRBM_GUI_ACTIVE per XCD / launch time of the profiled pass; busy_pmc = "
                                     "rocprofv3 VALUBusy of the profiled launch"}
         except Exception:
@@ -576,7 +603,7 @@ def main(argv=None):
         from qamr.pipeline import SofteningPipeline
 
         kstats = kernel_stats() if prof else {}
-        roof = roofline(args, w, kstats, w.dev) if (prof and rank == 0) else None
+        roof = roofline(args, w, kstats, w.dev, world) if (prof and rank == 0) else None
         it_mean = w.mean_iterations()
         # whole-decode algorithmic bandwidth (SURVEY.md 8(d) B_frame at the iterations actually run)
         B_frame = 16 * w.V + w.C + it_mean * (24 * w.E + 24 * w.V + w.C)

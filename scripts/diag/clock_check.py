@@ -3,12 +3,14 @@ unprofiled, from the in-kernel stamps of a QR_EXPERIMENT_CLOCK build (decoder.hi
 workgroup adds its s_memtime / s_memrealtime spans to g_clk), beside the launch time from
 hipEvents, for the default two-stream schedule and any QAMR_TUNE-style variants.
 
-  scripts/exp_build.sh clk "-DQR_EXPERIMENT_CLOCK=1"
-  QAMR_LIB=qam-reconciliation_amd/qamr/exp/libqamr_clk.so python scripts/diag/clock_check.py "" "split=1"
+  make -C qam-reconciliation_amd/csrc   (builds qamr/libqamr_clock.so beside libqamr.so)
+  QAMR_LIB=qam-reconciliation_amd/qamr/libqamr_clock.so python scripts/diag/clock_check.py "" "split=1"
 
 Per variant: step ms, check_d7 launch us (events), effective clock GHz, and the VALU issue
 fraction at that clock (1.585e9 wave-instructions x 4 cycles / 1024 SIMDs per 2048-frame
-launch, scaled by the launch's frames)."""
+launch, scaled by the launch's frames).
+  --json [--workload W --batch B]: one JSON line {"clock_ghz", "launch_us", "workgroups"} for
+the default tuning (QAMR_TUNE applies), read by bench.py's roofline."""
 import ctypes as C
 import os
 import sys
@@ -26,7 +28,7 @@ from qamr import _lib  # noqa: E402
 VALU_PER_FRAME = 1.585e9 / 2048  # wave-instructions of one check_d7 launch per frame (PMC, r03)
 
 
-def run(variant, w, L, steps=4):
+def run(variant, w, L, steps=4, quiet=False):
     for item in filter(None, variant.split(",")):
         k, v = item.split("=")
         _lib.tune_set(k.strip(), int(v))
@@ -50,6 +52,8 @@ def run(variant, w, L, steps=4):
     launch_us = ms / max(n, 1) * 1e3
     frames = w.B if _lib.tune_get("split") < 2 else w.B // 2
     issue_us = VALU_PER_FRAME * frames * 4 / 1024 / (ghz * 1e3)
+    if quiet:
+        return {"clock_ghz": round(ghz, 4), "launch_us": round(launch_us, 1), "workgroups": blocks, "steps": steps}
     print(f"variant '{variant or 'default'}': step {dt * 1e3:.1f} ms, {w.B / dt:.0f} frames/s, check_d7 "
           f"{launch_us:.0f} us x {n}, clock {ghz:.3f} GHz ({blocks} workgroups), VALU issue {issue_us:.0f} us "
           f"= {issue_us / launch_us:.3f} of the launch", flush=True)
@@ -58,13 +62,26 @@ def run(variant, w, L, steps=4):
 def main():
     L = _lib.load()
     L.qr_debug_clock.argtypes = [C.c_void_p]
+    argv = sys.argv[1:]
+    as_json = "--json" in argv
+    opts = {"--workload": "dvbs2_4pam", "--batch": "4096"}
+    for k in opts:
+        if k in argv:
+            i = argv.index(k)
+            opts[k] = argv[i + 1]
+            del argv[i:i + 2]
+    argv = [a for a in argv if a != "--json"]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    w = bench.Work("dvbs2_4pam", None, 4096, 50, 1.0, 0, 0, 0)
+    w = bench.Work(opts["--workload"], None, int(opts["--batch"]), 50, 1.0, 0, 0, 0)
     w.step_eager()
     w.sync()
+    if as_json:
+        import json
+        print(json.dumps(run("", w, L, quiet=True)), flush=True)
+        return
     defaults = {k: _lib.tune_get(k) for k in ("split", "check_per", "check_ft", "var_pace", "var_per")}
-    for variant in sys.argv[1:] or [""]:
+    for variant in argv or [""]:
         for k, v in defaults.items():
             _lib.tune_set(k, v)
         run(variant, w, L)
