@@ -157,6 +157,13 @@ struct CheckArgs {
     const int32_t *alist;   // active-frame list (frame ids at alist[f_off + p]) or null
     const int32_t *acount;  // its length
     const int32_t *finite;  // strict arithmetic: 1 iff the batch's input LAPPRs are all finite (or null)
+    // Short-tail grid (knob check_tail; k_check only): a 1-D grid whose first nmain blocks sweep
+    // frame tiles 1.. with g.per checks per thread (block b: tile 1 + b / nbx, check block
+    // b % nbx) and whose last blocks sweep frame tile 0 with per_t checks per thread -- the
+    // workgroups dispatched last are the short ones, so the launch drains in ~a quarter of a
+    // workgroup's time.  nmain = 0: the plain 2-D grid (nbx x frame tiles).
+    unsigned nmain;
+    int per_t;
 };
 
 // One variable sweep over the frame columns [f_off, f_off + ny*ft).
@@ -395,7 +402,7 @@ __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m
 // in the others; a wave whose lanes agree runs one path only (the other is skipped
 // under an empty exec mask), and a frame's result never depends on its wave-mates.
 template <int D, int MODE, bool NT, int AR, bool FIN = false, bool GL = false>
-__device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, unsigned by,
+__device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, unsigned by, int per,
                                             const typename Arith<AR>::Tab &tab, double *hb,
                                             uint32_t *pgb = nullptr) {
     const int ft = 1 << a.g.lft;
@@ -409,7 +416,7 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
     // messages are never read again and their posteriors (the output) are not touched.
     const bool act = a.active[f] != 0;
     if (!wave_any(act)) return;
-    int64_t ci = (int64_t)bx * a.g.per * nsub + sub;
+    int64_t ci = (int64_t)bx * per * nsub + sub;
     if (ci >= a.n_checks) return;
     uint32_t bad = 0;
     const auto K = Arith<AR>::regs();
@@ -422,9 +429,9 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
         double *wb = hb + (threadIdx.x >> 6) * kPackWaveStride;
         const uint32_t b8 = (uint32_t)f * 8u;
         constexpr int CL = FIN ? kClampFinite : kClampFull;
-        for (int j = 0; j < a.g.per; j += 2) {
+        for (int j = 0; j < per; j += 2) {
             if (ci >= a.n_checks) break;
-            const bool two = (j + 1 < a.g.per) && ci + nsub < a.n_checks;  // wave-uniform
+            const bool two = (j + 1 < per) && ci + nsub < a.n_checks;  // wave-uniform
             CheckIn<D, MODE, NT> x[2];
             double m[2][D];
             x[0].load(a, ci, f);
@@ -468,7 +475,7 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
     uint32_t *pg = GL ? pgb + (threadIdx.x >> 6) * (D * 128) : nullptr;
     if constexpr (GL) nx.load_glds(a, ci, f, pg);
     else nx.load(a, ci, f);
-    for (int j = 0; j < a.g.per; ++j) {
+    for (int j = 0; j < per; ++j) {
         // consume check j's inputs (m, parity) before its registers take check j+1's
         if constexpr (GL) nx.read_glds(pg);
         nx.load_c(a, f);
@@ -483,7 +490,7 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
         }
         struct { int base; uint8_t sb; } cur = {nx.base, nx.sb};
         const int64_t cn = ci + nsub;
-        const bool more = (j + 1 < a.g.per) && cn < a.n_checks;   // wave-uniform
+        const bool more = (j + 1 < per) && cn < a.n_checks;   // wave-uniform
         if constexpr (GL) {
             if (more) nx.load_glds(a, cn, f, pg);   // the reads above have completed (m uses them)
         } else if (kPrefetch && more) {
@@ -562,6 +569,10 @@ __device__ __forceinline__ void var_block(const VarArgs &a, unsigned bx, unsigne
 #endif
 #if QR_EXPERIMENT_CLOCK
 __device__ unsigned long long g_clk[3];
+// realtime start / end of every workgroup of the last such launch (up to kWgTimes workgroups):
+// the launch's occupancy over time, i.e. how much of it is the drain at its end
+constexpr int kWgTimes = 1 << 16;
+__device__ unsigned long long g_wgt[2 * kWgTimes];
 struct ClkScope {
     bool on;
     uint64_t c0, r0;
@@ -576,6 +587,11 @@ struct ClkScope {
             atomicAdd(&g_clk[0], (unsigned long long)(c1 - c0));
             atomicAdd(&g_clk[1], (unsigned long long)(r1 - r0));
             atomicAdd(&g_clk[2], 1ull);
+            const unsigned b = blockIdx.y * gridDim.x + blockIdx.x;
+            if (b < (unsigned)kWgTimes) {
+                g_wgt[2 * b] = r0;
+                g_wgt[2 * b + 1] = r1;
+            }
         }
     }
 };
@@ -587,18 +603,30 @@ k_check(CheckArgs a) {
     __shared__ typename Arith<AR>::Tab tab;
     __shared__ double hb[PackLds<AR>::doubles];
     __shared__ uint32_t pgb[GL ? 4 * D * 128 : 1];   // 4 waves x D posterior rows (LDS DMA)
-    if (!frames_block_live(a.acount, blockIdx.y, a.g.lft)) return;  // block-uniform
+    unsigned bx = blockIdx.x, by = blockIdx.y;
+    int per = a.g.per;
+    if (a.nmain) {  // short-tail 1-D grid (block-uniform)
+        if (bx < a.nmain) {
+            by = 1 + bx / a.nbx;
+            bx -= (by - 1) * a.nbx;
+        } else {
+            bx -= a.nmain;
+            by = 0;
+            per = a.per_t;
+        }
+    }
+    if (!frames_block_live(a.acount, by, a.g.lft)) return;  // block-uniform
 #if QR_EXPERIMENT_CLOCK
     ClkScope clk(D == 7 && MODE == kNormal && AR == kStrict);
 #endif
     if (MODE != kParityOnly) stage_tables<AR>(&tab, a);
     if constexpr (AR == kStrict && MODE != kParityOnly && QR_STRICT_FINITE && QR_STRICT_PACK && D <= kPackMaxDeg) {
         if (a.finite && sld(a.finite)) {  // kernel-uniform: one of the two bodies runs
-            check_block<D, MODE, NT, AR, true, GL>(a, blockIdx.x, blockIdx.y, tab, hb, pgb);
+            check_block<D, MODE, NT, AR, true, GL>(a, bx, by, per, tab, hb, pgb);
             return;
         }
     }
-    check_block<D, MODE, NT, AR, false, GL>(a, blockIdx.x, blockIdx.y, tab, hb, pgb);
+    check_block<D, MODE, NT, AR, false, GL>(a, bx, by, per, tab, hb, pgb);
 }
 
 // finite = 1 iff every LAPPR of frames [0, B) is below bound in magnitude (the flag was set
@@ -665,7 +693,7 @@ k_fused(CheckArgs ca, VarArgs va, unsigned nb_check, unsigned nb_total) {
     if (c1 > c0) {  // block-uniform branch
         if (!frames_block_live(ca.acount, c0 / ca.nbx, ca.g.lft)) return;
         stage_tables<AR>(&tab, ca);
-        check_block<D, MODE, NT, AR>(ca, c0 % ca.nbx, c0 / ca.nbx, tab, hb);
+        check_block<D, MODE, NT, AR>(ca, c0 % ca.nbx, c0 / ca.nbx, ca.g.per, tab, hb);
     } else {
         const unsigned vi = b - c0;
         if (!frames_block_live(va.acount, vi / va.nbx, va.g.lft)) return;
@@ -847,7 +875,8 @@ static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
 // Runtime tuning knobs (qr_tune_set); defaults picked by scripts/tune.py on MI355X.
 struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3}, math{kStrict}, eps_max{40},
-        lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024}, var_pace{28};
+        lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024}, var_pace{28},
+        check_tail{0};
 };
 static Tuning g_tune;
 
@@ -884,7 +913,7 @@ struct Plan {
     hipStream_t s;
     int lds_pad = 0;  // dynamic LDS reserved by each check workgroup (caps their CU residency)
     bool compact = false;  // sweeps of the main loop read the active-frame lists
-    int var_pace = 0;      // variable sweeps: workgroups per frame tile (0 = one per tile)
+    int var_pace = 0;      // variable sweeps: workgroups per 128 frames (0 = one per tile)
 
     const int32_t *count_of(int f0) const { return w.acount + (f0 == 0 ? 0 : 1); }
 
@@ -912,6 +941,8 @@ struct Plan {
         a.fb_base = cls.fb_base;
         a.alist = a.acount = nullptr;
         a.finite = w.acount + 2;
+        a.nmain = 0;
+        a.per_t = a.g.per;
         return a;
     }
     VarArgs var_args(int f0, int f1) const {
@@ -959,6 +990,16 @@ static int launch_check_class(const Plan &P, const DegreeClass &cls, const doubl
     }
     const int ar = math_mode(MODE);
     dim3 grid(a.nbx, (unsigned)((f1 - f0) >> a.g.lft));
+    // knob check_tail (0 = off): frame tile 0 is swept last with per / check_tail
+    // checks per thread (the templated degrees only; the runtime-degree kernel keeps the 2-D grid)
+    const int tail = g_tune.check_tail.load();
+    if (tail > 1 && grid.y >= 2 && cls.degree <= kMaxTemplDeg && a.g.per >= tail) {
+        const int64_t per_block_t = (int64_t)(a.g.per / tail) * (256 >> a.g.lft);
+        const int64_t nbx_t = (cls.n + per_block_t - 1) / per_block_t;
+        a.nmain = a.nbx * (grid.y - 1);
+        a.per_t = a.g.per / tail;
+        grid = dim3((unsigned)(a.nmain + nbx_t), 1);
+    }
     ProfScope ps(profiling_on() ? std::string(MODE == kParityOnly ? "parity_d" : MODE == kFirst ? "check1_d" : "check_d") +
                                       std::to_string(cls.degree)
                                 : std::string(),
@@ -1003,10 +1044,10 @@ static int launch_var(const Plan &P, int f0, int f1) {
     }
     dim3 grid(a.nbx, a.nby);
     // Paced sweep (the two-stream schedule's variable sweeps, Plan::var_pace): at most var_pace
-    // workgroups per frame tile, each walking tiles grid-stride, so that the sweep streams its
+    // workgroups per 128 frames of the sweep, each walking its tiles grid-stride, so that the sweep streams its
     // bytes over about the length of the concurrent check sweep instead of saturating HBM for
     // the first ~40 % of it.
-    const int64_t cap = (int64_t)P.var_pace * a.nby;
+    const int64_t cap = (int64_t)P.var_pace * (((int64_t)a.nby << a.g.lft) / 128);  // per 128 frames
     if (cap > 0 && (int64_t)a.nbx * a.nby > cap) {
         a.gs = 1;
         grid = dim3((unsigned)cap, 1);
@@ -1154,7 +1195,7 @@ static int run_split(const Plan &P, int max_it) {
 // each SIMD and stream their messages under the check sweep's fp64 arithmetic (in
 // the fused launch they take whole check-sized slots instead): 5.15 vs 5.35 ms per
 // half-iteration for the strict arithmetic (MI355X, B=4096).  The variable sweeps are paced
-// (knob var_pace, workgroups per frame tile, default 28): unpaced, the sweep saturates HBM for
+// (knob var_pace, workgroups per 128 frames, default 28): unpaced, the sweep saturates HBM for
 // the first ~1.7 ms of the 4.3 ms check launch beside it and the check sweep's gathers stall
 // (VALU issue 0.72 of the launch); paced to stream over the whole check launch, 4.15 ms and
 // 0.85 (MI355X, B=4096: 8.96 k -> 9.70 k frames/s on one box).  Knob lds_pad_kb reserves
@@ -1181,17 +1222,26 @@ static int side_stream(const qr_code *code, hipStream_t *out) {
     return QR_OK;
 }
 
-static int run_split2(const Plan &P, int max_it) {
+static int run_split2(const Plan &P, int max_it, bool overlap = false) {
     const qr_code *code = P.code;
     std::lock_guard<std::mutex> lk(code->mu);
     hipStream_t s2 = nullptr;
     if (int rc0 = side_stream(code, &s2)) return rc0;
+    // split = 5: the check sweeps of half B on a third stream, so that C_A(t+1) (which needs
+    // only V_A(t)) may start while C_B(t) drains instead of after it
+    hipStream_t sB = P.s;
+    if (overlap) {
+        if (!code->s3) QR_HIP(hipStreamCreateWithFlags(&code->s3, hipStreamNonBlocking));
+        sB = code->s3;
+    }
     hipEvent_t fork = code->ev[0], cA = code->ev[1], cB = code->ev[2], vA = code->ev[3], vB = code->ev[4];
     Plan V = P;
     V.s = s2;
     V.var_pace = g_tune.var_pace.load();
     Plan C = P;
     C.lds_pad = std::max(0, g_tune.lds_pad_kb.load()) * 1024;
+    Plan CB = C, PB = P;  // half B's check-stream plans
+    CB.s = PB.s = sB;
     const int ld = P.ld, h = ld / 2;
     const int A0 = 0, A1 = h, B0 = h, B1 = ld;
     auto row = [&](int t) { return P.w.unsat + (size_t)t * ld; };
@@ -1207,11 +1257,11 @@ static int run_split2(const Plan &P, int max_it) {
     for (int k = 0; k < (int)code->classes.size(); ++k)
         if (k != big) side_edges += code->classes[k].n * code->classes[k].degree;
     const bool side = g_tune.side.load() && code->classes.size() > 1 && side_edges * 8 <= code->E;
-    auto checks_main = [&](int t, int f0, int f1) {  // check sweep t >= 2 on the check stream
-        if (!side) return launch_checks<kNormal>(C, P.post, row(t - 1), f0, f1);
+    auto checks_main = [&](const Plan &Q, int t, int f0, int f1) {  // check sweep t >= 2 on Q's stream
+        if (!side) return launch_checks<kNormal>(Q, P.post, row(t - 1), f0, f1);
         const DegreeClass &cls = code->classes[big];
-        return P.nt ? launch_check_class<kNormal, true>(C, cls, P.post, row(t - 1), f0, f1)
-                    : launch_check_class<kNormal, false>(C, cls, P.post, row(t - 1), f0, f1);
+        return P.nt ? launch_check_class<kNormal, true>(Q, cls, P.post, row(t - 1), f0, f1)
+                    : launch_check_class<kNormal, false>(Q, cls, P.post, row(t - 1), f0, f1);
     };
     auto checks_side = [&](int t, int f0, int f1) {  // the other classes of check sweep t, on V.s
         return side ? launch_checks<kNormal>(V, P.post, row(t - 1), f0, f1, big) : (int)QR_OK;
@@ -1219,6 +1269,7 @@ static int run_split2(const Plan &P, int max_it) {
     int rc;
     QR_HIP(hipEventRecord(fork, P.s));
     QR_HIP(hipStreamWaitEvent(V.s, fork, 0));
+    if (sB != P.s) QR_HIP(hipStreamWaitEvent(sB, fork, 0));
     if ((rc = launch_checks<kFirst>(C, P.post, row(0), A0, A1))) return rc;
     QR_HIP(hipEventRecord(cA, P.s));
     for (int t = 1; t <= max_it; ++t) {
@@ -1227,16 +1278,16 @@ static int run_split2(const Plan &P, int max_it) {
         if (t < max_it && (rc = checks_side(t + 1, A0, A1))) return rc;
         QR_HIP(hipEventRecord(vA, V.s));
         if (t == 1) {
-            if ((rc = launch_checks<kFirst>(C, P.post, row(0), B0, B1))) return rc;
+            if ((rc = launch_checks<kFirst>(CB, P.post, row(0), B0, B1))) return rc;
         } else {
-            QR_HIP(hipStreamWaitEvent(P.s, vB, 0));
-            if ((rc = checks_main(t, B0, B1))) return rc;
-            if ((rc = launch_status_compact(P, B0, B1, t - 1, row(t - 1)))) return rc;
+            QR_HIP(hipStreamWaitEvent(sB, vB, 0));
+            if ((rc = checks_main(CB, t, B0, B1))) return rc;
+            if ((rc = launch_status_compact(PB, B0, B1, t - 1, row(t - 1)))) return rc;
         }
-        QR_HIP(hipEventRecord(cB, P.s));
+        QR_HIP(hipEventRecord(cB, sB));
         if (t < max_it) {
             QR_HIP(hipStreamWaitEvent(P.s, vA, 0));
-            if ((rc = checks_main(t + 1, A0, A1))) return rc;
+            if ((rc = checks_main(C, t + 1, A0, A1))) return rc;
             if ((rc = launch_status_compact(P, A0, A1, t, row(t)))) return rc;
             QR_HIP(hipEventRecord(cA, P.s));
         }
@@ -1245,7 +1296,7 @@ static int run_split2(const Plan &P, int max_it) {
         if (t < max_it && (rc = checks_side(t + 1, B0, B1))) return rc;
         QR_HIP(hipEventRecord(vB, V.s));
     }
-    // join: everything after (final parity check, status) follows both sweeps
+    // join: everything after (final parity check, status) follows both sweeps (vB follows cB)
     QR_HIP(hipStreamWaitEvent(P.s, vA, 0));
     QR_HIP(hipStreamWaitEvent(P.s, vB, 0));
     return QR_OK;
@@ -1343,8 +1394,8 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     } else if ((rc = launch_compact(P, 0, ld))) {
         return rc;
     }
-    if ((rc = !split ? run_flat(P, max_it) : sp >= 4 ? run_pipes(P, max_it) : sp == 3 ? run_split2(P, max_it)
-                                                                           : run_split(P, max_it)))
+    if ((rc = !split ? run_flat(P, max_it) : sp == 5 ? run_split2(P, max_it, true) : sp >= 4 ? run_pipes(P, max_it)
+                                                   : sp == 3 ? run_split2(P, max_it) : run_split(P, max_it)))
         return rc;
     // Check after the last sweep; then every frame still running stops with (0, max).
     const int tf = max_it > 0 ? max_it : 0;
@@ -1438,6 +1489,7 @@ static int free_code(qr_code *c) {
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->s2) (void)hipStreamDestroy(c->s2);
+    if (c->s3) (void)hipStreamDestroy(c->s3);
     delete c;
     return QR_OK;
 }
@@ -1523,6 +1575,12 @@ QR_API int qr_debug_clock(int64_t *out) {
     for (int i = 0; i < 3; ++i) out[i] = (int64_t)h[i];
     return QR_OK;
 }
+// out[2 n]: realtime {start, end} of workgroups 0..n-1 of the last stamped launch
+QR_API int qr_debug_wg_times(int64_t *out, int32_t n) {
+    if (n < 0 || n > qr::kWgTimes) return QR_EVALUE;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(qr::g_wgt), (size_t)n * 16) != hipSuccess) return QR_EDEVICE;
+    return QR_OK;
+}
 #endif
 
 // name -> knob (nullptr if unknown)
@@ -1536,7 +1594,7 @@ static std::atomic<int> *tune_knob(const char *name) {
         {"side", &g_tune.side},             {"demap_fast", &g_demap_fast},
         {"demap_hyp", &g_demap_hyp},        {"min_blocks", &g_tune.min_blocks},
         {"split_min_blocks", &g_tune.split_min_blocks},
-        {"var_pace", &g_tune.var_pace},
+        {"var_pace", &g_tune.var_pace},     {"check_tail", &g_tune.check_tail},
     };
     const std::string n = name ? name : "";
     for (const auto &k : knobs)

@@ -59,6 +59,38 @@ def run(variant, w, L, steps=4, quiet=False):
           f"= {issue_us / launch_us:.3f} of the launch", flush=True)
 
 
+def wg_times(w, L, steps=2):
+    """Occupancy of the last stamped check_d7 launch over time: how many of its workgroups are
+    resident, and how long the drain at its end lasts."""
+    import numpy as np
+
+    for _ in range(steps):
+        w.step_eager()
+    w.sync()
+    L.qr_debug_wg_times.argtypes = [C.c_void_p, C.c_int32]
+    nb = 1 << 16
+    buf = (C.c_int64 * (2 * nb))()
+    L.qr_debug_wg_times(buf, nb)
+    t = np.frombuffer(buf, dtype=np.int64).reshape(nb, 2)
+    t = t[(t[:, 0] > 0) & (t[:, 1] >= t[:, 0])]
+    t0 = t[:, 0].min()
+    s, e = (t[:, 0] - t0) * 10e-3, (t[:, 1] - t0) * 10e-3  # us (100 MHz ticks)
+    span = e.max()
+    grid = np.linspace(0, span, 2001)
+    active = np.array([np.count_nonzero((s <= x) & (e > x)) for x in grid])
+    peak = np.percentile(active, 90)
+    busy = (e - s).sum()
+    below = grid[active < 0.9 * peak]
+    drain = span - below[below > span / 2].min() if np.any(below > span / 2) else 0.0
+    print(f"workgroups {len(t)}, span {span:.0f} us, workgroup duration median {np.median(e - s):.0f} us "
+          f"(p10 {np.percentile(e - s, 10):.0f}, p90 {np.percentile(e - s, 90):.0f}), resident peak {peak:.0f}, "
+          f"mean {busy / span:.0f} = {busy / span / peak:.3f} of peak; drain (below 90 % of peak) {drain:.0f} us; "
+          f"first start spread {np.percentile(s, 5):.0f} us", flush=True)
+    for q in (0.5, 0.8, 0.9, 0.95, 0.98):
+        x = grid[int(q * 2000)]
+        print(f"  t = {x:7.0f} us: {np.count_nonzero((s <= x) & (e > x))} resident", flush=True)
+
+
 def main():
     L = _lib.load()
     L.qr_debug_clock.argtypes = [C.c_void_p]
@@ -70,7 +102,7 @@ def main():
             i = argv.index(k)
             opts[k] = argv[i + 1]
             del argv[i:i + 2]
-    argv = [a for a in argv if a != "--json"]
+    argv = [a for a in argv if a not in ("--json",)]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     w = bench.Work(opts["--workload"], None, int(opts["--batch"]), 50, 1.0, 0, 0, 0)
@@ -80,8 +112,12 @@ def main():
         import json
         print(json.dumps(run("", w, L, quiet=True)), flush=True)
         return
-    defaults = {k: _lib.tune_get(k) for k in ("split", "check_per", "check_ft", "var_pace", "var_per")}
-    for variant in argv or [""]:
+    if "--wgtimes" in argv:
+        wg_times(w, L)
+        return
+    defaults = {k: _lib.tune_get(k) for k in ("split", "check_per", "check_ft", "var_pace", "var_per", "var_ft", "nt", "compact",
+                                             "side", "lds_pad_kb", "check_tail")}
+    for variant in [a for a in argv if a != "--wgtimes"] or [""]:
         for k, v in defaults.items():
             _lib.tune_set(k, v)
         run(variant, w, L)
