@@ -876,7 +876,7 @@ static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
 struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3}, math{kStrict}, eps_max{40},
         lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024}, var_pace{28},
-        check_tail{0};
+        check_tail{4};
 };
 static Tuning g_tune;
 
@@ -990,7 +990,7 @@ static int launch_check_class(const Plan &P, const DegreeClass &cls, const doubl
     }
     const int ar = math_mode(MODE);
     dim3 grid(a.nbx, (unsigned)((f1 - f0) >> a.g.lft));
-    // knob check_tail (0 = off): frame tile 0 is swept last with per / check_tail
+    // knob check_tail (default 4; 0 = off; MI355X: +1 %): frame tile 0 is swept last with per / check_tail
     // checks per thread (the templated degrees only; the runtime-degree kernel keeps the 2-D grid)
     const int tail = g_tune.check_tail.load();
     if (tail > 1 && grid.y >= 2 && cls.degree <= kMaxTemplDeg && a.g.per >= tail) {
