@@ -316,7 +316,7 @@ def kernel_clock(args):
     import subprocess
 
     lib = os.path.join(ROOT, "qam-reconciliation_amd", "qamr", "libqamr_clock.so")
-    if not os.path.exists(lib):
+    if not os.path.exists(lib) or os.environ.get("QAMR_NO_CLOCK_PASS") == "1":  # (set under rocprofv3)
         return None
     cmd = [sys.executable, os.path.join(ROOT, "scripts", "diag", "clock_check.py"), "--json",
            "--workload", args.workload, "--batch", str(args.batch)]

@@ -4,6 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
+export QAMR_NO_CLOCK_PASS=1  # bench.py: no child clock pass under the profiler
 OUT=gpurun_out/prof_${TAG:-r1}
 mkdir -p "$OUT"
 BENCH=${BENCH:-"bench.py"}
