@@ -179,6 +179,11 @@ struct VarArgs {
     const int32_t *alist, *acount;  // as CheckArgs
     unsigned nby;  // frame tiles (grid-stride launches)
     int gs;        // 1: a capped 1-D grid walks the nbx x nby tiles (the paced sweeps of run_split2, knob var_pace)
+    // INIT sweep only: the strict arithmetic's finite flag (QR_STRICT_FINITE) is cleared when an
+    // input LAPPR of a frame < fin_B is not below fin_bound in magnitude (null: not computed)
+    int32_t *finite;
+    double fin_bound;
+    int fin_B;
 };
 
 // Active-frame compaction (converging operating points, decoder.pyx:431-433: frames stop
@@ -301,7 +306,7 @@ struct CheckIn {
 // update runs there.
 constexpr int kPackMaxDeg = 10;
 // QR_STRICT_FINITE (default 1): when every input LAPPR of the batch's frames is below a bound
-// 2^e (a device flag computed at the start of the decode, k_finite), no inf or NaN can arise
+// 2^e (a device flag computed by the decode's first variable sweep), no inf or NaN can arise
 // in any sweep: |c2v| <= max |v2c| (a box-plus never exceeds its smaller operand, to
 // rounding) and |v2c| <= |L| + (dv - 1) max |c2v|, so X_t = max |post| + max |c2v| after
 // sweep t obeys X_{t+1} <= |L| + (dv + 1) X_t and every value (box-plus arguments, twice
@@ -542,18 +547,21 @@ __device__ __forceinline__ void var_block(const VarArgs &a, unsigned bx, unsigne
     const bool act = a.active[f] != 0;
     if (!live || (!INIT && !act)) return;
     const int64_t v0 = (int64_t)bx * a.g.per * nsub + sub;
+    bool big = false;
     for (int j = 0; j < a.g.per; ++j) {
         const int64_t v = v0 + (int64_t)j * nsub;
         if (v >= a.V) break;
         const int b = sld(a.var_ptr + v), e = sld(a.var_ptr + v + 1);
         double p = ld_msg<NT>(&a.lappr[(size_t)v * ld + f]);
         if (INIT) {
+            big |= !(__builtin_fabs(p) < a.fin_bound);
             if (act && e > b) p = p + 0.0;
         } else {
             for (int k = b; k < e; ++k) p += ld_msg<NT>(&a.c2v[(size_t)sld(a.var_edge + k) * ld + f]);
         }
         a.post[(size_t)v * ld + f] = p;
     }
+    if (INIT && a.finite && big && f < a.fin_B) *a.finite = 0;  // every writer stores 0
 }
 
 #ifndef QR_CHECK_STRICT_WAVES
@@ -627,17 +635,6 @@ k_check(CheckArgs a) {
         }
     }
     check_block<D, MODE, NT, AR, false, GL>(a, bx, by, per, tab, hb, pgb);
-}
-
-// finite = 1 iff every LAPPR of frames [0, B) is below bound in magnitude (the flag was set
-// to 1 by k_init_status; every thread that sees a larger, infinite or NaN value stores 0).
-__global__ void __launch_bounds__(256) k_finite(const double *__restrict__ lappr, int64_t V, int ld, int B,
-                                                double bound, int32_t *finite) {
-    bool bad = false;
-    for (int64_t r = blockIdx.y; r < V; r += gridDim.y)
-        for (int f = blockIdx.x * 256 + threadIdx.x; f < B; f += gridDim.x * 256)
-            bad |= !(__builtin_fabs(lappr[r * ld + f]) < bound);
-    if (bad) *finite = 0;
 }
 
 template <bool INIT, bool NT>
@@ -844,7 +841,7 @@ struct DecodeWs {
     double *fb;      // F scratch of the runtime-degree classes (fb_rows rows of ld), or null
     int32_t *alist;  // active-frame lists of the frame ranges (ld entries)
     int32_t *acount; // their lengths: [0] range starting at frame 0, [1] the second half;
-                     // [2] the finite flag of the input LAPPRs (k_finite)
+                     // [2] the finite flag of the input LAPPRs (first variable sweep)
 };
 
 static size_t ws_bytes(const qr_code *code, int ld, int max_it) {
@@ -962,6 +959,9 @@ struct Plan {
         a.alist = a.acount = nullptr;
         a.nby = (unsigned)((f1 - f0) >> a.g.lft);
         a.gs = 0;
+        a.finite = nullptr;
+        a.fin_bound = 0.0;
+        a.fin_B = 0;
         return a;
     }
 };
@@ -1035,9 +1035,12 @@ static int launch_checks(const Plan &P, const double *post_in, uint8_t *unsat, i
 }
 
 template <bool INIT>
-static int launch_var(const Plan &P, int f0, int f1) {
+static int launch_var(const Plan &P, int f0, int f1, int32_t *finite = nullptr, double fin_bound = 0.0) {
     ProfScope ps(INIT ? "var_init" : "var", P.s);
     VarArgs a = P.var_args(f0, f1);
+    a.finite = finite;
+    a.fin_bound = fin_bound;
+    a.fin_B = P.B;
     if (P.compact && !INIT) {
         a.alist = P.w.alist;
         a.acount = P.count_of(f0);
@@ -1361,19 +1364,14 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     // (in double, clamped before the cast: max_it may be as large as INT_MAX)
     const double fin_x = ((double)std::max(max_it, 0) + 2.0) * std::log2((double)code->max_dv + 1.0);
     const int fin_e = fin_x > 999.0 ? 0 : 1000 - (int)std::ceil(fin_x);
-    if (fin_e < 1) {
-        QR_HIP(hipMemsetAsync(P.w.acount + 2, 0, sizeof(int32_t), s));
-    } else if (g_tune.math.load() == kStrict) {
-        const unsigned gx = (unsigned)std::min(16, (B + 255) / 256);
-        k_finite<<<dim3(gx, (unsigned)std::min<int64_t>(code->V, 4096 / gx)), 256, 0, s>>>(
-            lappr, code->V, ld, B, std::ldexp(1.0, fin_e), P.w.acount + 2);
-        QR_LAUNCH_CHECK();
-    }
+    if (fin_e < 1) QR_HIP(hipMemsetAsync(P.w.acount + 2, 0, sizeof(int32_t), s));
+    // the flag itself is computed by the first variable sweep, which reads every LAPPR anyway
+    int32_t *fin_flag = (fin_e >= 1 && g_tune.math.load() == kStrict) ? P.w.acount + 2 : nullptr;
     // decoder.pyx:400-405: the input itself may already satisfy the syndrome.
     if ((rc = launch_checks<kParityOnly>(P, lappr, P.w.unsat, 0, ld))) return rc;
     if ((rc = launch_status(P, 0, ld, 0, 0, 0, P.w.unsat))) return rc;
     // decoder.pyx:408-421: c2v = 0, first variable sweep.
-    if ((rc = launch_var<true>(P, 0, ld))) return rc;
+    if ((rc = launch_var<true>(P, 0, ld, fin_flag, fin_flag ? std::ldexp(1.0, fin_e) : 0.0))) return rc;
     int max_deg = 0;
     int64_t max_n = 0;
     for (const auto &c : code->classes) max_deg = std::max(max_deg, c.degree), max_n = std::max(max_n, c.n);
