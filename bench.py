@@ -149,8 +149,8 @@ class StubWork:
     """CPU stand-in for the GPU step (QAMR_BENCH_STUB=1): exercises the launcher,
     the timed region and the counter reduction of the real rank body."""
 
-    def __init__(self, args, rank):
-        self.args, self.rank = args, rank
+    def __init__(self, args, rank, local):
+        self.args, self.rank, self.local = args, rank, local
         self.B = args.batch
         self.V, self.C, self.E = 1008, 504, 3024
         self.dev = None  # host tensors (qamr.dist stages them for a GPU-only backend)
@@ -214,10 +214,16 @@ class Work:
         graph; step() then replays it (no per-launch host overhead)."""
         import torch
 
-        self.step_eager()  # allocates the decode workspace outside the capture
+        # The decode workspace is keyed by the launch stream (qamr.Decoder): warm up on the stream
+        # the capture will use, so the captured step reuses that allocation instead of allocating
+        # a second ~E x ld x 8 B workspace from the graph pool.
+        s = torch.cuda.Stream(self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(s):
+            self.step_eager()
         torch.cuda.synchronize(self.dev)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph, stream=s):
             self.step_eager()
         torch.cuda.synchronize(self.dev)
 
@@ -409,11 +415,9 @@ def roofline(args, w, kstats, dev, world=1):
                             "source": t.get("source"),
                             "note": "SIMD issue time of the launch's VALU instructions (4 cycles per wave64 "
                                     "instruction, counts from profiles/pmc_traffic.json, rocprofv3 --pmc) at the "
-                                    "shader clock the check launches run at (s_memtime / s_memrealtime spans of "
-                                    "their workgroups in an unprofiled pass of the diagnostic twin library), over "
-                                    "the live launch time; clock_ghz_pmc = "
-                                    "GRBM_GUI_ACTIVE per XCD / launch time of the profiled pass; busy_pmc = "
-                                    "rocprofv3 VALUBusy of the profiled launch"}
+                                    "shader clock named by clock_source, over the live launch time; "
+                                    "clock_ghz_pmc = GRBM_GUI_ACTIVE per XCD / launch time of the profiled pass; "
+                                    "busy_pmc = rocprofv3 VALUBusy of the profiled launch"}
         except Exception:
             traffic = None
     copy_gbps = copy_bandwidth(dev)
@@ -548,7 +552,7 @@ def main(argv=None):
     import torch
 
     if stub:
-        w = StubWork(args, rank)
+        w = StubWork(args, rank, local)
     else:
         import qamr
 
@@ -586,6 +590,11 @@ def main(argv=None):
     elapsed = timed_region(w.step, w.sync, args.steps, args.warmup, before, after, device=w.dev)
     counters = w.counters()
     dist.all_reduce_sum(counters)
+    # the GPU each rank bound (LOCAL_RANK, or QAMR_BENCH_DEVICE in a rehearsal), gathered on rank 0
+    bound = torch.zeros(world, dtype=torch.int64, device=w.dev)
+    bound[rank] = 1 + (w.local if stub else torch.cuda.current_device())
+    dist.all_reduce_sum(bound)
+    rank_devices = [int(v) - 1 for v in bound.cpu().numpy()]
     total_frames = world * w.B * args.steps
     value = total_frames / elapsed
 
@@ -597,7 +606,7 @@ def main(argv=None):
     }
     if stub:
         out["config"] = {"workload": "stub", "batch_per_gpu": w.B, "global_batch": world * w.B,
-                         "parallelism": f"dp{world}", "backend": dist.backend()}
+                         "parallelism": f"dp{world}", "backend": dist.backend(), "rank_devices": rank_devices}
         out["counters"] = [int(v) for v in counters]
     else:
         from qamr.pipeline import SofteningPipeline
@@ -616,7 +625,7 @@ def main(argv=None):
                          "batch_per_gpu": w.B, "global_batch": world * w.B, "max_iterations": args.max_iter,
                          "snr_db": w.snr, "bps": w.bps, "fused_demap": w.fused, "parallelism": f"dp{world}",
                          "hip_graph": graph,
-                         "backend": dist.backend() or "none",
+                         "backend": dist.backend() or "none", "rank_devices": rank_devices,
                          "arithmetic": args.math + (" (glibc exp/log restated: outputs bit-identical to the "
                                                     "reference)" if args.math == "strict" else
                                                     " (approximate, opt-in)")}

@@ -156,6 +156,21 @@ QR_API int qr_demap_batch_device(const qr_demap *dm, int32_t B, int32_t ld, int6
 /* NoiseMapper.demap_lappr_array for one array from host memory: lappr[S*bps]. */
 QR_API int qr_demap_host(const qr_demap *dm, int64_t S, const double *n, const int64_t *j, double *lappr);
 
+/* NoiseMapper.g_inv_search (noisemapper.pyx:310-345) over arrays, i.e.
+ * NoiseMapper.demap_noise_search (noisemapper.pyx:407-419): y_hat[k] = the root of
+ * F_Y(y) = target(n_hat[k], i[k]) by the reference's doubling bracket + bisection to
+ * hi - lo <= y_accuracy (default 1e-9 in the reference).  Bit-identical to the
+ * reference.  i[k] outside [0, M) gives NaN (out-of-bounds reads in the reference);
+ * the bracket + bisection loops are capped at 2200 steps (NaN), where the reference
+ * loops forever (targets outside [0, 1], y_accuracy below the spacing of the doubles
+ * near the root).  Host arrays of n elements; synchronous. */
+QR_API int qr_g_inv_search_host(const qr_demap *dm, int64_t n, const double *n_hat, const int64_t *i,
+                                double y_accuracy, double *y_hat);
+/* NoiseMapper.F_Y (noisemapper.pyx:264-275): F[k] = (sum_m F_Z(y[k], a_m, sigma)) / M, the
+ * uniformly weighted mixture CDF (the cpdef ignores the alphabet's probabilities).  Host
+ * arrays of n elements; synchronous. */
+QR_API int qr_F_Y_host(const qr_demap *dm, int64_t n, const double *y, double *F);
+
 /* ---------------------------------------------- softening pipeline (Bob) */
 /* NoiseMapper.hard_decide_index + map_noise (noisemapper.pyx:349-388) and
  * PAMAlphabet.demap_symbols_to_bits (alphabet.pyx:98-107), fused, frame-innermost:

@@ -59,6 +59,8 @@ def lib():
     L.orc_nm_tables.argtypes = [vp, _f64p, _f64p, _f64p, _f64p]
     L.orc_single_F_Y.argtypes = [vp, C.c_double]
     L.orc_single_F_Y.restype = C.c_double
+    L.orc_public_F_Y.argtypes = [vp, C.c_double]
+    L.orc_public_F_Y.restype = C.c_double
     L.orc_g_inv_search.argtypes = [vp, C.c_double, C.c_int, C.c_double, C.POINTER(C.c_int64)]
     L.orc_g_inv_search.restype = C.c_double
     L.orc_demap_lappr_array.argtypes = [vp, _f64p, _i64p, C.c_int64, _f64p, C.c_int]
@@ -192,6 +194,9 @@ class OracleNoiseMapper:
 
     def single_F_Y(self, y):
         return lib().orc_single_F_Y(self._h, float(y))
+
+    def F_Y(self, y):
+        return np.array([lib().orc_public_F_Y(self._h, float(v)) for v in np.asarray(y, np.float64).ravel()])
 
     def g_inv_search(self, n_hat, i, y_accuracy=1e-9):
         ev = C.c_int64(0)

@@ -336,6 +336,13 @@ static inline double single_F_Y(const orc_nm *nm, double y) {
 }
 double orc_single_F_Y(const orc_nm *nm, double y) { return single_F_Y(nm, y); }
 
+/* noisemapper.pyx:264-275 (cpdef F_Y): uniform weighting, divided by the order */
+double orc_public_F_Y(const orc_nm *nm, double y) {
+    double res = F_Z(y, nm->a[0], nm->den);
+    for (int i = 1; i < nm->M; ++i) res += F_Z(y, nm->a[i], nm->den);
+    return res / nm->M;
+}
+
 /* alphabet.pyx:35-76 (constellation :62, thresholds :69-73) and
  * noisemapper.pyx:103-162 (sigma :132, F_Y_thresholds :149-153, delta_F_Y :159-162).
  * probabilities == NULL -> uniform 1/M (alphabet.pyx:46-47);

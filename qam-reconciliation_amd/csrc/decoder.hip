@@ -88,10 +88,7 @@ __device__ __forceinline__ T sld(const T *p) {
 // the (wave-uniform) row pointer in scalar registers: the lane's byte offset goes in the
 // instruction's VGPR offset, so an access costs no VALU (a flat/global access needs a
 // 64-bit v_lshl_add per access here, the compiler hoists base + lane offset and adds the
-// scalar row offset per access).  QR_BUFFER_MSG=0: plain loads/stores.
-#ifndef QR_BUFFER_MSG
-#define QR_BUFFER_MSG 1
-#endif
+// scalar row offset per access).
 typedef unsigned int qr_u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const double *rowp, int ld) {
     // word 3 = 0x00020000: DATA_FORMAT 32 (raw dword access), no swizzle; num_records = row bytes
@@ -112,19 +109,11 @@ __device__ __forceinline__ T *at_byte(T *rowp, uint32_t boff) {
 // Load / store of the lane's double in a wave-uniform row (row pointer rowp, ld doubles).
 template <bool NT>
 __device__ __forceinline__ double ld_row(const double *rowp, uint32_t b8, int ld) {
-#if QR_BUFFER_MSG
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(row_rsrc(rowp, ld), b8, 0, NT ? 2 : 0));
-#else
-    return ld_msg<NT>(at_byte(rowp, b8));
-#endif
 }
 template <bool NT>
 __device__ __forceinline__ void st_row(double *rowp, uint32_t b8, int ld, double v) {
-#if QR_BUFFER_MSG
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(qr_u32x2, v), row_rsrc(rowp, ld), b8, 0, NT ? 2 : 0);
-#else
-    st_msg<NT>(at_byte(rowp, b8), v);
-#endif
 }
 
 // Block geometry shared by the check and variable sweeps: 256 threads = `ft`
@@ -179,7 +168,7 @@ struct VarArgs {
     const int32_t *alist, *acount;  // as CheckArgs
     unsigned nby;  // frame tiles (grid-stride launches)
     int gs;        // 1: a capped 1-D grid walks the nbx x nby tiles (the paced sweeps of run_split2, knob var_pace)
-    // INIT sweep only: the strict arithmetic's finite flag (QR_STRICT_FINITE) is cleared when an
+    // INIT sweep only: the strict arithmetic's finite flag (see kPackMaxDeg) is cleared when an
     // input LAPPR of a frame < fin_B is not below fin_bound in magnitude (null: not computed)
     int32_t *finite;
     double fin_bound;
@@ -211,32 +200,9 @@ __device__ __forceinline__ void stage_tables(typename Arith<AR>::Tab *lds, const
 }
 
 // The inputs of one check update: gathered posteriors, own c2v messages, syndrome bit.
-// Prefetch depth: the gathered posteriors of check j+1 are always issued before the
-// arithmetic of check j; its own (streamed, row-contiguous) messages are loaded on
-// use unless QR_PREFETCH_C=1 -- 14 fewer live VGPRs, 3.19 vs 3.25 ms per launch.
-#ifndef QR_PREFETCH_C
-#define QR_PREFETCH_C 0
-#endif
-// QR_CHECK_PREFETCH=0: the gathers of check j+1 are issued after the arithmetic of
-// check j instead of before it (fewer live VGPRs, no latency hiding of its own).
-#ifndef QR_CHECK_PREFETCH
-#define QR_CHECK_PREFETCH 1
-#endif
-#ifndef QR_PACK_PREFETCH
-#define QR_PACK_PREFETCH 0
-#endif
-// QR_CHECK_GLDS: the packed strict check sweep gathers the next check's posteriors by LDS DMA
-// (buffer_load_dword ... lds) right after it has consumed the current check's inputs, so the
-// gathers of check j+1 are in flight during the arithmetic of check j without holding VGPRs.
-#ifndef QR_CHECK_GLDS
-#define QR_CHECK_GLDS 0
-#endif
-#ifndef QR_LOAD_BEFORE_STORE
-#define QR_LOAD_BEFORE_STORE 0
-#endif
-#ifndef QR_STORE_RECOMPUTE
-#define QR_STORE_RECOMPUTE 0
-#endif
+// The gathered posteriors of check j+1 are issued before the arithmetic of check j on the
+// unpacked paths (the packed strict update needs those registers: with the prefetch it runs
+// at 3 waves/SIMD, 142 VGPRs); the own (streamed, row-contiguous) messages are loaded on use.
 template <int D, int MODE, bool NT>
 struct CheckIn {
     double p[D], c[D];
@@ -249,137 +215,54 @@ struct CheckIn {
         base = sld(a.chk_ptr + cc);
         sb = *at_byte(row_ptr(a.synd, cc, ld), (uint32_t)f);
 #pragma unroll
-        for (int i = 0; i < D; ++i) {
-            p[i] = ld_row<false>(row_ptr(a.post, sld(a.chk_var + base + i), ld), b8, ld);
-            if (MODE == kNormal && QR_PREFETCH_C) c[i] = ld_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), ld), b8, ld);
-        }
-    }
-    // LDS-DMA flavour (QR_CHECK_GLDS): the D gathered posterior rows go straight into this
-    // wave's LDS buffer pg (D x 128 dwords: the lanes' low dwords, then their high dwords,
-    // row after row -- buffer_load_dword ... lds writes lane-linear), no VGPR holds them
-    // in flight; the syndrome byte stays an ordinary load.
-    __device__ __forceinline__ void load_glds(const CheckArgs &a, int64_t ci, int f, uint32_t *pg) {
-        const int ld = a.ld;
-        const uint32_t b8 = (uint32_t)f * 8u;
-        const int cc = sld(a.checks + ci);
-        base = sld(a.chk_ptr + cc);
-        sb = *at_byte(row_ptr(a.synd, cc, ld), (uint32_t)f);
-#pragma unroll
-        for (int i = 0; i < D; ++i) {
-            const __amdgpu_buffer_rsrc_t r = row_rsrc(row_ptr(a.post, sld(a.chk_var + base + i), ld), ld);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)(pg + i * 128), 4,
-                                                    b8, 0, 0, 0);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)(pg + i * 128 + 64),
-                                                    4, b8 + 4u, 0, 0, 0);
-        }
-    }
-    // Wait for the DMA (the compiler does not track it: an explicit vmcnt(0), which is also a
-    // compiler memory barrier so the LDS reads stay below it), then read back.
-    __device__ __forceinline__ void read_glds(const uint32_t *pg) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t lane = __lane_id();
-#pragma unroll
-        for (int i = 0; i < D; ++i) {
-            const uint32_t *q = pg + i * 128;
-            p[i] = __builtin_bit_cast(double, ((uint64_t)q[64 + lane] << 32) | q[lane]);
-        }
+        for (int i = 0; i < D; ++i) p[i] = ld_row<false>(row_ptr(a.post, sld(a.chk_var + base + i), ld), b8, ld);
     }
     __device__ __forceinline__ void load_c(const CheckArgs &a, int f) {
-        if (MODE != kNormal || QR_PREFETCH_C) return;
+        if (MODE != kNormal) return;
         const uint32_t b8 = (uint32_t)f * 8u;
 #pragma unroll
         for (int i = 0; i < D; ++i) c[i] = ld_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), a.ld), b8, a.ld);
     }
 };
 
-// decoder.pyx:322-369 for one check with the box-plus of Arith<AR>:
-// F[i] = bp(F[i-1], m[i]); the backward values B[i] = bp(B[i+1], m[i]) are consumed as
-// they are produced (out_i = bp(F[i-1], B[i+1])): the same operands as
-// decoder.pyx:341-367, one live B instead of D.  Lane byte offset b8 = f * 8.
-// QR_STRICT_PACK (default 1): the strict update runs the two glibc log paths on full
-// wavefronts (strict_pack.hpp); 0: the sequential loops below, log branch per lane.
-#ifndef QR_STRICT_PACK
-#define QR_STRICT_PACK 1
-#endif
 // Degrees whose round loop the compiler still unrolls fully (above, the packed update's
 // register arrays would be indexed dynamically, i.e. live in scratch): the unpacked strict
 // update runs there.
 constexpr int kPackMaxDeg = 10;
-// QR_STRICT_FINITE (default 1): when every input LAPPR of the batch's frames is below a bound
-// 2^e (a device flag computed by the decode's first variable sweep), no inf or NaN can arise
-// in any sweep: |c2v| <= max |v2c| (a box-plus never exceeds its smaller operand, to
+// The strict arithmetic's finite flag: when every input LAPPR of the batch's frames is below
+// a bound 2^e (a device flag computed by the decode's first variable sweep), no inf or NaN can
+// arise in any sweep: |c2v| <= max |v2c| (a box-plus never exceeds its smaller operand, to
 // rounding) and |v2c| <= |L| + (dv - 1) max |c2v|, so X_t = max |post| + max |c2v| after
 // sweep t obeys X_{t+1} <= |L| + (dv + 1) X_t and every value (box-plus arguments, twice
 // that) stays below 2^e (dv + 1)^(max_it + 2), which e = 1000 - (max_it + 2) log2(dv_max + 1)
-// keeps finite.  The check
-// sweeps then run the packed update with the one-instruction clamp (strict_pack.hpp
-// kClampFinite) instead of the NaN-preserving two-instruction one.
-// QR_STRICT_UNCLAMPED (default 0): within those sweeps, waves whose check inputs are all
-// below 350 in magnitude run without any clamp (two code paths in the loop: more VGPRs).
-#ifndef QR_STRICT_FINITE
-#define QR_STRICT_FINITE 1
-#endif
-#ifndef QR_STRICT_UNCLAMPED
-#define QR_STRICT_UNCLAMPED 0
-#endif
-// QR_PACK_PAIR: each thread updates two checks per loop step with their log arguments packed
-// together (strict_pack.hpp check_strict_packed_n<D, CL, 2>): one partly filled slice per kind
-// and round for both checks instead of one each.
-#ifndef QR_PACK_PAIR
-#define QR_PACK_PAIR 0
-#endif
-constexpr int kPackPairMaxDeg = 8;
-// LDS of the packed strict update: one buffer per wavefront of a block (64 lanes x the
-// arguments of one round, + one slice of slack).
-constexpr int kPackWaveStride = QR_PACK_PAIR ? 64 * 2 * kPackMaxJobs + 64 : kPackWaveDoubles;
+// keeps finite.  The check sweeps then run the packed update with the one-instruction clamp
+// (strict_pack.hpp kClampFinite) instead of the NaN-preserving two-instruction one.
+// LDS of the packed strict update: one buffer per wavefront of a block.
 template <int AR>
 struct PackLds {
-    static constexpr int doubles = (AR == kStrict && QR_STRICT_PACK) ? 4 * kPackWaveStride : 1;
+    static constexpr int doubles = AR == kStrict ? 4 * kPackWaveDoubles : 1;
 };
+template <int AR, int D>
+constexpr bool kPacked = AR == kStrict && D <= kPackMaxDeg;
 
-struct NoPre {
-    __device__ __forceinline__ void operator()() const {}
-};
-// pre(): called in the packed path after the outputs are computed and before they are stored
-// (QR_LOAD_BEFORE_STORE: the next check's loads are issued ahead of this check's stores, so the
-// wait for them does not include the stores' completion -- gfx9 counts both in vmcnt).
-template <int AR, int D, bool NT, bool FIN = false, class Pre = NoPre>
+// decoder.pyx:322-369 for one check with the box-plus of Arith<AR>.
+// Packed strict update (D <= kPackMaxDeg): strict_pack.hpp.  Otherwise
+// F[i] = bp(F[i-1], m[i]); the backward values B[i] = bp(B[i+1], m[i]) are consumed as
+// they are produced (out_i = bp(F[i-1], B[i+1])): the same operands as
+// decoder.pyx:341-367, one live B instead of D.  Lane byte offset b8 = f * 8.
+template <int AR, int D, bool NT, bool FIN = false>
 __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m)[D], int base, uint8_t sb, uint32_t b8,
                                             const typename Arith<AR>::Tab &tab, const typename Arith<AR>::Regs &K,
-                                            double *hb = nullptr, bool live = true, Pre pre = Pre{}) {
+                                            double *hb = nullptr, bool live = true) {
     const int ld = a.ld;
     const double s = sb ? -1.0 : 1.0;
-    if constexpr (AR == kStrict && QR_STRICT_PACK && D <= kPackMaxDeg) {
+    if constexpr (kPacked<AR, D>) {
         double out[D];
-        double *wb = hb + (threadIdx.x >> 6) * kPackWaveStride;
-        if constexpr (FIN) {
-#if QR_STRICT_UNCLAMPED
-            // Every h argument of the check is |F +- m|, |B +- m| or |F +- B|, and |F|, |B| <=
-            // max |m_i| (the box-plus magnitude never exceeds min(|a|, |b|), to rounding), so
-            // inputs below 350 keep every argument below 700: the wave runs the update
-            // without a clamp when all its lanes qualify.
-            bool small = true;
+        double *wb = hb + (threadIdx.x >> 6) * kPackWaveDoubles;
+        check_strict_packed<D, FIN ? kClampFinite : kClampFull>(m, out, wb, tab, K);
 #pragma unroll
-            for (int i = 0; i < D; ++i) small &= __builtin_fabs(m[i]) < 350.0;
-            if (__ballot(!small) == 0) check_strict_packed<D, kClampNone>(m, out, wb, tab, K);
-            else check_strict_packed<D, kClampFinite>(m, out, wb, tab, K);
-#else
-            check_strict_packed<D, kClampFinite>(m, out, wb, tab, K);
-#endif
-        } else {
-            check_strict_packed<D, kClampFull>(m, out, wb, tab, K);
-        }
-        pre();
-#pragma unroll
-        for (int i = 0; i < D; ++i) {
-            int e = sld(a.chk_edge + base + i);
-#if QR_STORE_RECOMPUTE
-            // a fresh value for the compiler: the store's row pointer and buffer resource are
-            // rebuilt here (a few SALU) instead of held in SGPRs across the whole update
-            asm volatile("" : "+s"(e));
-#endif
-            if (live) st_row<NT>(row_ptr(a.c2v, e, ld), b8, ld, s * out[i]);
-        }
+        for (int i = 0; i < D; ++i)
+            if (live) st_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), ld), b8, ld, s * out[i]);
         return;
     }
     double F[D - 1];
@@ -399,20 +282,17 @@ __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m
 
 // One lane = one (check, frame); each thread walks `per` checks of one degree class.
 // decoder.pyx:322-369 (F/B recursion) with the parity test of decoder.pyx:235-257
-// fused on the posteriors it gathers anyway.  Software-pipelined: the posterior
-// gathers of check j+1 are issued before the box-plus arithmetic of check j, so
-// each wave keeps its own loads in flight under its VALU work.
+// fused on the posteriors it gathers anyway.  Unpacked paths are software-pipelined: the
+// posterior gathers of check j+1 are issued before the box-plus arithmetic of check j.
 // EPS: the update runs in the exp domain (fastmath.hpp::check_node_eps, ~2.4x fewer
 // VALU instructions) in every lane whose inputs are all in its domain, the exact path
 // in the others; a wave whose lanes agree runs one path only (the other is skipped
 // under an empty exec mask), and a frame's result never depends on its wave-mates.
-template <int D, int MODE, bool NT, int AR, bool FIN = false, bool GL = false>
+template <int D, int MODE, bool NT, int AR, bool FIN = false>
 __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, unsigned by, int per,
-                                            const typename Arith<AR>::Tab &tab, double *hb,
-                                            uint32_t *pgb = nullptr) {
+                                            const typename Arith<AR>::Tab &tab, double *hb) {
     const int ft = 1 << a.g.lft;
     const int nsub = 256 >> a.g.lft;
-    const int ld = a.ld;
     bool live;
     const int f = lane_frame(a.alist, a.acount, a.f_off, (int)(by << a.g.lft) + (threadIdx.x & (ft - 1)), live);
     const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> a.g.lft);
@@ -425,64 +305,11 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
     if (ci >= a.n_checks) return;
     uint32_t bad = 0;
     const auto K = Arith<AR>::regs();
-    // The packed strict update needs the registers the prefetched gathers would hold:
-    // with them it runs at 3 waves/SIMD (142 VGPRs) or spills at 4; without, 4 waves and
-    // 4.54 vs 4.96 ms per launch (MI355X, configs[2]).
-    constexpr bool kPrefetch = QR_CHECK_PREFETCH && (QR_PACK_PREFETCH || !(AR == kStrict && QR_STRICT_PACK));
-    if constexpr (QR_PACK_PAIR && AR == kStrict && QR_STRICT_PACK && MODE != kParityOnly && D <= kPackPairMaxDeg) {
-        // two checks per step (ci, ci + nsub); a lone last check takes the single update
-        double *wb = hb + (threadIdx.x >> 6) * kPackWaveStride;
-        const uint32_t b8 = (uint32_t)f * 8u;
-        constexpr int CL = FIN ? kClampFinite : kClampFull;
-        for (int j = 0; j < per; j += 2) {
-            if (ci >= a.n_checks) break;
-            const bool two = (j + 1 < per) && ci + nsub < a.n_checks;  // wave-uniform
-            CheckIn<D, MODE, NT> x[2];
-            double m[2][D];
-            x[0].load(a, ci, f);
-            if (two) x[1].load(a, ci + nsub, f);
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                if (c == 1 && !two) break;
-                x[c].load_c(a, f);
-                uint32_t par = x[c].sb;
-#pragma unroll
-                for (int i = 0; i < D; ++i) {
-                    const double p = x[c].p[i];
-                    if (MODE != kFirst) par ^= (p < 0.0) ? 1u : 0u;   // decoder.pyx:243-246
-                    m[c][i] = (MODE == kNormal) ? p - x[c].c[i] : p;   // :296-297
-                }
-                if (MODE != kFirst) bad |= (par == 1u) ? 1u : 0u;
-            }
-            if (two) {
-                double out[2][D];
-                check_strict_packed_n<D, CL, 2>(m, out, wb, tab, K);
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    const double sg = x[c].sb ? -1.0 : 1.0;
-#pragma unroll
-                    for (int i = 0; i < D; ++i)
-                        if (live) st_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + x[c].base + i), ld), b8, ld, sg * out[c][i]);
-                }
-            } else {
-                check_exact<AR, D, NT, FIN>(a, m[0], x[0].base, x[0].sb, b8, tab, K, hb, live);
-            }
-            ci += 2 * nsub;
-        }
-        if (MODE != kFirst && bad && act && live) a.unsat[f] = 1;
-        return;
-    }
-    // the next check's loads issued between this check's arithmetic and its stores (packed
-    // strict update only: its outputs are all in registers at that point)
-    constexpr bool kLoadBeforeStore = QR_LOAD_BEFORE_STORE && !kPrefetch && !GL && MODE != kParityOnly &&
-                                      AR == kStrict && QR_STRICT_PACK && D <= kPackMaxDeg;
+    constexpr bool kPrefetch = !kPacked<AR, D>;
     CheckIn<D, MODE, NT> nx;
-    uint32_t *pg = GL ? pgb + (threadIdx.x >> 6) * (D * 128) : nullptr;
-    if constexpr (GL) nx.load_glds(a, ci, f, pg);
-    else nx.load(a, ci, f);
+    nx.load(a, ci, f);
     for (int j = 0; j < per; ++j) {
         // consume check j's inputs (m, parity) before its registers take check j+1's
-        if constexpr (GL) nx.read_glds(pg);
         nx.load_c(a, f);
         uint32_t par = nx.sb;
         double m[D];
@@ -496,11 +323,7 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
         struct { int base; uint8_t sb; } cur = {nx.base, nx.sb};
         const int64_t cn = ci + nsub;
         const bool more = (j + 1 < per) && cn < a.n_checks;   // wave-uniform
-        if constexpr (GL) {
-            if (more) nx.load_glds(a, cn, f, pg);   // the reads above have completed (m uses them)
-        } else if (kPrefetch && more) {
-            nx.load(a, cn, f);
-        }
+        if (kPrefetch && more) nx.load(a, cn, f);
         if (MODE != kFirst) bad |= (par == 1u) ? 1u : 0u;  // satisfied iff (parity ^ 1) != 0
         if (MODE != kParityOnly) {
             const uint32_t b8 = (uint32_t)f * 8u;
@@ -512,21 +335,17 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
                 if (in || !act) {  // stopped lanes never force the exact path
                     const int base = cur.base;
                     check_node_eps<D>(m, cur.sb, tab, [&](int i, double v) {
-                        if (live) st_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), ld), b8, ld, v);
+                        if (live) st_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), a.ld), b8, a.ld, v);
                     });
                 } else {
                     check_exact<kFast, D, NT>(a, m, cur.base, cur.sb, b8, tab, Arith<kFast>::Regs{}, nullptr, live);
                 }
-            } else if constexpr (kLoadBeforeStore) {
-                check_exact<AR, D, NT, FIN>(a, m, cur.base, cur.sb, b8, tab, K, hb, live, [&]() {
-                    if (more) nx.load(a, cn, f);
-                });
             } else {
                 check_exact<AR, D, NT, FIN>(a, m, cur.base, cur.sb, b8, tab, K, hb, live);
             }
         }
         if (!more) break;
-        if (!kPrefetch && !GL && !kLoadBeforeStore) nx.load(a, cn, f);
+        if (!kPrefetch) nx.load(a, cn, f);
         ci = cn;
     }
     if (MODE != kFirst && bad && act && live) a.unsat[f] = 1;  // benign race: every writer stores 1
@@ -564,9 +383,6 @@ __device__ __forceinline__ void var_block(const VarArgs &a, unsigned bx, unsigne
     if (INIT && a.finite && big && f < a.fin_B) *a.finite = 0;  // every writer stores 0
 }
 
-#ifndef QR_CHECK_STRICT_WAVES
-#define QR_CHECK_STRICT_WAVES 1
-#endif
 // QR_EXPERIMENT_CLOCK (diagnostic builds only, scripts/diag/clock_check.py): every workgroup of
 // the degree-7 main-loop check sweep stamps the shader clock (s_memtime) and the 100 MHz
 // realtime counter around its work and adds both spans to g_clk (vector atomics); the effective
@@ -605,12 +421,9 @@ struct ClkScope {
 };
 #endif
 template <int D, int MODE, bool NT, int AR>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AR == kStrict ? QR_CHECK_STRICT_WAVES : 1, 8)))
-k_check(CheckArgs a) {
-    constexpr bool GL = QR_CHECK_GLDS && AR == kStrict && QR_STRICT_PACK && D <= kPackMaxDeg;
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) k_check(CheckArgs a) {
     __shared__ typename Arith<AR>::Tab tab;
     __shared__ double hb[PackLds<AR>::doubles];
-    __shared__ uint32_t pgb[GL ? 4 * D * 128 : 1];   // 4 waves x D posterior rows (LDS DMA)
     unsigned bx = blockIdx.x, by = blockIdx.y;
     int per = a.g.per;
     if (a.nmain) {  // short-tail 1-D grid (block-uniform)
@@ -628,13 +441,13 @@ k_check(CheckArgs a) {
     ClkScope clk(D == 7 && MODE == kNormal && AR == kStrict);
 #endif
     if (MODE != kParityOnly) stage_tables<AR>(&tab, a);
-    if constexpr (AR == kStrict && MODE != kParityOnly && QR_STRICT_FINITE && QR_STRICT_PACK && D <= kPackMaxDeg) {
+    if constexpr (MODE != kParityOnly && kPacked<AR, D>) {
         if (a.finite && sld(a.finite)) {  // kernel-uniform: one of the two bodies runs
-            check_block<D, MODE, NT, AR, true, GL>(a, bx, by, per, tab, hb, pgb);
+            check_block<D, MODE, NT, AR, true>(a, bx, by, per, tab, hb);
             return;
         }
     }
-    check_block<D, MODE, NT, AR, false, GL>(a, bx, by, per, tab, hb, pgb);
+    check_block<D, MODE, NT, AR, false>(a, bx, by, per, tab, hb);
 }
 
 template <bool INIT, bool NT>
@@ -989,7 +802,8 @@ static int launch_check_class(const Plan &P, const DegreeClass &cls, const doubl
         a.acount = P.count_of(f0);
     }
     const int ar = math_mode(MODE);
-    dim3 grid(a.nbx, (unsigned)((f1 - f0) >> a.g.lft));
+    const dim3 grid2(a.nbx, (unsigned)((f1 - f0) >> a.g.lft));   // the plain 2-D grid
+    dim3 grid = grid2;
     // knob check_tail (default 4; 0 = off; MI355X: +1 %): frame tile 0 is swept last with per / check_tail
     // checks per thread (the templated degrees only; the runtime-degree kernel keeps the 2-D grid)
     const int tail = g_tune.check_tail.load();
@@ -1013,9 +827,11 @@ static int launch_check_class(const Plan &P, const DegreeClass &cls, const doubl
     bool handled = true;
     QR_DEG_SWITCH(cls.degree, QR_CASE, handled)
 #undef QR_CASE
-    if (!handled) {
-        if (ar == kStrict) k_check_generic<MODE, kStrict><<<grid, 256, 0, P.s>>>(a);
-        else k_check_generic<MODE, kFast><<<grid, 256, 0, P.s>>>(a);
+    if (!handled) {  // the runtime-degree kernel decodes its frame tile from blockIdx.y: 2-D grid only
+        a.nmain = 0;
+        a.per_t = a.g.per;
+        if (ar == kStrict) k_check_generic<MODE, kStrict><<<grid2, 256, 0, P.s>>>(a);
+        else k_check_generic<MODE, kFast><<<grid2, 256, 0, P.s>>>(a);
     }
     QR_LAUNCH_CHECK();
     return QR_OK;
@@ -1225,26 +1041,17 @@ static int side_stream(const qr_code *code, hipStream_t *out) {
     return QR_OK;
 }
 
-static int run_split2(const Plan &P, int max_it, bool overlap = false) {
+static int run_split2(const Plan &P, int max_it) {
     const qr_code *code = P.code;
     std::lock_guard<std::mutex> lk(code->mu);
     hipStream_t s2 = nullptr;
     if (int rc0 = side_stream(code, &s2)) return rc0;
-    // split = 5: the check sweeps of half B on a third stream, so that C_A(t+1) (which needs
-    // only V_A(t)) may start while C_B(t) drains instead of after it
-    hipStream_t sB = P.s;
-    if (overlap) {
-        if (!code->s3) QR_HIP(hipStreamCreateWithFlags(&code->s3, hipStreamNonBlocking));
-        sB = code->s3;
-    }
     hipEvent_t fork = code->ev[0], cA = code->ev[1], cB = code->ev[2], vA = code->ev[3], vB = code->ev[4];
     Plan V = P;
     V.s = s2;
     V.var_pace = g_tune.var_pace.load();
     Plan C = P;
     C.lds_pad = std::max(0, g_tune.lds_pad_kb.load()) * 1024;
-    Plan CB = C, PB = P;  // half B's check-stream plans
-    CB.s = PB.s = sB;
     const int ld = P.ld, h = ld / 2;
     const int A0 = 0, A1 = h, B0 = h, B1 = ld;
     auto row = [&](int t) { return P.w.unsat + (size_t)t * ld; };
@@ -1272,7 +1079,6 @@ static int run_split2(const Plan &P, int max_it, bool overlap = false) {
     int rc;
     QR_HIP(hipEventRecord(fork, P.s));
     QR_HIP(hipStreamWaitEvent(V.s, fork, 0));
-    if (sB != P.s) QR_HIP(hipStreamWaitEvent(sB, fork, 0));
     if ((rc = launch_checks<kFirst>(C, P.post, row(0), A0, A1))) return rc;
     QR_HIP(hipEventRecord(cA, P.s));
     for (int t = 1; t <= max_it; ++t) {
@@ -1281,13 +1087,13 @@ static int run_split2(const Plan &P, int max_it, bool overlap = false) {
         if (t < max_it && (rc = checks_side(t + 1, A0, A1))) return rc;
         QR_HIP(hipEventRecord(vA, V.s));
         if (t == 1) {
-            if ((rc = launch_checks<kFirst>(CB, P.post, row(0), B0, B1))) return rc;
+            if ((rc = launch_checks<kFirst>(C, P.post, row(0), B0, B1))) return rc;
         } else {
-            QR_HIP(hipStreamWaitEvent(sB, vB, 0));
-            if ((rc = checks_main(CB, t, B0, B1))) return rc;
-            if ((rc = launch_status_compact(PB, B0, B1, t - 1, row(t - 1)))) return rc;
+            QR_HIP(hipStreamWaitEvent(P.s, vB, 0));
+            if ((rc = checks_main(C, t, B0, B1))) return rc;
+            if ((rc = launch_status_compact(P, B0, B1, t - 1, row(t - 1)))) return rc;
         }
-        QR_HIP(hipEventRecord(cB, sB));
+        QR_HIP(hipEventRecord(cB, P.s));
         if (t < max_it) {
             QR_HIP(hipStreamWaitEvent(P.s, vA, 0));
             if ((rc = checks_main(C, t + 1, A0, A1))) return rc;
@@ -1302,45 +1108,6 @@ static int run_split2(const Plan &P, int max_it, bool overlap = false) {
     // join: everything after (final parity check, status) follows both sweeps (vB follows cB)
     QR_HIP(hipStreamWaitEvent(P.s, vA, 0));
     QR_HIP(hipStreamWaitEvent(P.s, vB, 0));
-    return QR_OK;
-}
-
-// Two independent pipelines (split = 4): the frame halves A and B share no data, so each
-// runs its own in-order sequence  C(1) | V(1) C(2) S(1) | V(2) C(3) S(2) | ...  on its own
-// stream (A on the caller's, B on the second), with no cross-stream event inside the loop:
-// the GPU interleaves the two, and one half's launch tail is filled by the other half's
-// work instead of an event wait.  Per frame the order is exactly run_split's.
-static int run_pipes(const Plan &P, int max_it) {
-    const qr_code *code = P.code;
-    std::lock_guard<std::mutex> lk(code->mu);
-    hipStream_t s2 = nullptr;
-    if (int rc0 = side_stream(code, &s2)) return rc0;
-    hipEvent_t fork = code->ev[0], join = code->ev[4];
-    const int ld = P.ld, h = ld / 2;
-    auto row = [&](int t) { return P.w.unsat + (size_t)t * ld; };
-    Plan PB = P;
-    PB.s = s2;
-    QR_HIP(hipEventRecord(fork, P.s));
-    QR_HIP(hipStreamWaitEvent(PB.s, fork, 0));
-    int rc;
-    for (int half = 0; half < 2; ++half) {
-        const Plan &Q = half ? PB : P;
-        const int f0 = half ? h : 0, f1 = half ? ld : h;
-        if ((rc = launch_checks<kFirst>(Q, P.post, row(0), f0, f1))) return rc;
-    }
-    for (int t = 1; t <= max_it; ++t) {
-        for (int half = 0; half < 2; ++half) {   // enqueue order only: the streams run freely
-            const Plan &Q = half ? PB : P;
-            const int f0 = half ? h : 0, f1 = half ? ld : h;
-            if ((rc = launch_var<false>(Q, f0, f1))) return rc;
-            if (t < max_it) {
-                if ((rc = launch_checks<kNormal>(Q, P.post, row(t), f0, f1))) return rc;
-                if ((rc = launch_status_compact(Q, f0, f1, t, row(t)))) return rc;
-            }
-        }
-    }
-    QR_HIP(hipEventRecord(join, PB.s));
-    QR_HIP(hipStreamWaitEvent(P.s, join, 0));
     return QR_OK;
 }
 
@@ -1360,7 +1127,7 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     QR_HIP(hipMemsetAsync(P.w.unsat, 0, (size_t)rows * ld, s));
     k_init_status<<<(ld + 255) / 256, 256, 0, s>>>(B, ld, P.w.active, success, iters, P.w.acount + 2);
     QR_LAUNCH_CHECK();
-    // the finite flag (QR_STRICT_FINITE): bound 2^e with e = 1000 - (max_it + 2) log2(dv_max + 1)
+    // the strict arithmetic's finite flag: bound 2^e with e = 1000 - (max_it + 2) log2(dv_max + 1)
     // (in double, clamped before the cast: max_it may be as large as INT_MAX)
     const double fin_x = ((double)std::max(max_it, 0) + 2.0) * std::log2((double)code->max_dv + 1.0);
     const int fin_e = fin_x > 999.0 ? 0 : 1000 - (int)std::ceil(fin_x);
@@ -1392,8 +1159,7 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     } else if ((rc = launch_compact(P, 0, ld))) {
         return rc;
     }
-    if ((rc = !split ? run_flat(P, max_it) : sp == 5 ? run_split2(P, max_it, true) : sp >= 4 ? run_pipes(P, max_it)
-                                                   : sp == 3 ? run_split2(P, max_it) : run_split(P, max_it)))
+    if ((rc = !split ? run_flat(P, max_it) : sp == 3 ? run_split2(P, max_it) : run_split(P, max_it)))
         return rc;
     // Check after the last sweep; then every frame still running stops with (0, max).
     const int tf = max_it > 0 ? max_it : 0;
@@ -1487,7 +1253,6 @@ static int free_code(qr_code *c) {
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->s2) (void)hipStreamDestroy(c->s2);
-    if (c->s3) (void)hipStreamDestroy(c->s3);
     delete c;
     return QR_OK;
 }
@@ -1603,7 +1368,8 @@ static std::atomic<int> *tune_knob(const char *name) {
 int qr_tune_set(const char *name, int64_t value) {
     std::atomic<int> *k = tune_knob(name);
     if (!k) return set_error(QR_EVALUE, "unknown tuning knob '%s'", name ? name : "");
-    if (value < 0 || value > 4096) return set_error(QR_EVALUE, "tuning value out of range");
+    if (value < 0 || value > 4096 || (k == &g_tune.split && value > 3))
+        return set_error(QR_EVALUE, "tuning value out of range");
     k->store((int)value);
     return QR_OK;
 }

@@ -361,6 +361,33 @@ __global__ void __launch_bounds__(256) k_map_noise(const DemapTables *__restrict
     nhat[s * ld + f] = g;
 }
 
+// noisemapper.pyx:310-345 (cpdef g_inv_search) over arrays, i.e. :407-419 (demap_noise_search):
+// y_hat[k] = g_inv_search(n_hat[k], i[k], y_accuracy).  At the default accuracy 1e-9 the fast
+// certified search runs (bit-identical to the reference's loops: tests/test_demap_replay.py);
+// any other accuracy runs the loops verbatim.  An out-of-range i gives NaN (the reference
+// indexes sign_config / F_Y_thresholds out of bounds).
+__global__ void __launch_bounds__(256) k_g_inv_search(const DemapTables *__restrict__ tab,
+                                                      const MathTables *__restrict__ gmt, int64_t n,
+                                                      const double *__restrict__ n_hat, const int64_t *__restrict__ idx,
+                                                      double y_accuracy, int fast, double *__restrict__ y_hat) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const DemapTables &t = *tab;
+    const int64_t i = idx[k];
+    double y;
+    if (i < 0 || i >= t.M) y = __builtin_nan("");
+    else if (fast && y_accuracy == 1e-9) y = g_inv_search_fast(t, *gmt, n_hat[k], (int)i);
+    else y = g_inv_search(t, n_hat[k], (int)i, y_accuracy);
+    y_hat[k] = y;
+}
+
+// noisemapper.pyx:264-275 (cpdef F_Y, uniform weighting).
+__global__ void __launch_bounds__(256) k_public_F_Y(const DemapTables *__restrict__ tab, int64_t n,
+                                                    const double *__restrict__ y, double *__restrict__ F) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) F[k] = public_F_Y(*tab, y[k]);
+}
+
 // matrix.pyx:55-60, frame-innermost; one lane = (check, frame).
 __global__ void __launch_bounds__(256) k_syndrome(int64_t C, int ld, int B, const int32_t *__restrict__ chk_ptr,
                                                   const int32_t *__restrict__ chk_var,
@@ -558,6 +585,50 @@ int qr_demap_host(const qr_demap *dm, int64_t S, const double *n, const int64_t 
         QR_LAUNCH_CHECK();
     }
     QR_HIP(hipMemcpy(lappr, d_l, S * bps * 8, hipMemcpyDeviceToHost));
+    return QR_OK;
+}
+
+int qr_g_inv_search_host(const qr_demap *dm, int64_t n, const double *n_hat, const int64_t *i, double y_accuracy,
+                         double *y_hat) {
+    if (!dm) return set_error(QR_EVALUE, "null demapper");
+    if (n < 0) return set_error(QR_EVALUE, "negative size");
+    if (n == 0) return QR_OK;
+    if (!n_hat || !i || !y_hat) return set_error(QR_EVALUE, "null pointer argument");
+    DeviceGuard g(dm->device);
+    std::lock_guard<std::mutex> lk(dm->scratch.mu);
+    const size_t a = align_up((size_t)n * 8, 256);
+    int rc = dm->scratch.reserve(3 * a);
+    if (rc) return rc;
+    char *p = (char *)dm->scratch.ptr;
+    double *d_n = (double *)p;
+    int64_t *d_i = (int64_t *)(p + a);
+    double *d_y = (double *)(p + 2 * a);
+    QR_HIP(hipMemcpy(d_n, n_hat, (size_t)n * 8, hipMemcpyHostToDevice));
+    QR_HIP(hipMemcpy(d_i, i, (size_t)n * 8, hipMemcpyHostToDevice));
+    k_g_inv_search<<<(unsigned)((n + 255) / 256), 256>>>(dm->d_tables, dm->d_mtab, n, d_n, d_i, y_accuracy,
+                                                         g_demap_fast.load() != 0, d_y);
+    QR_LAUNCH_CHECK();
+    QR_HIP(hipMemcpy(y_hat, d_y, (size_t)n * 8, hipMemcpyDeviceToHost));
+    return QR_OK;
+}
+
+int qr_F_Y_host(const qr_demap *dm, int64_t n, const double *y, double *F) {
+    if (!dm) return set_error(QR_EVALUE, "null demapper");
+    if (n < 0) return set_error(QR_EVALUE, "negative size");
+    if (n == 0) return QR_OK;
+    if (!y || !F) return set_error(QR_EVALUE, "null pointer argument");
+    DeviceGuard g(dm->device);
+    std::lock_guard<std::mutex> lk(dm->scratch.mu);
+    const size_t a = align_up((size_t)n * 8, 256);
+    int rc = dm->scratch.reserve(2 * a);
+    if (rc) return rc;
+    char *p = (char *)dm->scratch.ptr;
+    double *d_y = (double *)p;
+    double *d_F = (double *)(p + a);
+    QR_HIP(hipMemcpy(d_y, y, (size_t)n * 8, hipMemcpyHostToDevice));
+    k_public_F_Y<<<(unsigned)((n + 255) / 256), 256>>>(dm->d_tables, n, d_y, d_F);
+    QR_LAUNCH_CHECK();
+    QR_HIP(hipMemcpy(F, d_F, (size_t)n * 8, hipMemcpyDeviceToHost));
     return QR_OK;
 }
 

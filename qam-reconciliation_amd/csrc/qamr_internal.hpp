@@ -106,7 +106,6 @@ struct qr_code {
     // while a decode enqueues (concurrent decodes on one code enqueue one at a time).
     mutable std::mutex mu;
     mutable hipStream_t s2 = nullptr;
-    mutable hipStream_t s3 = nullptr;  // split = 5: the check sweeps of the second frame half
     mutable hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
 };
 

@@ -217,38 +217,12 @@ QR_HD int search_bracket(const SearchCmp &cmp, double &lo, double &hi) {
     return guard;
 }
 
-// search_bracket in closed form when the window is certified: the loop probes 2^m (up) or
-// -2^m (down), m = 0, 1, ..., and stops at the first probe quick() does not place on the
-// near side of ystar.  With z = ystar (up) or -ystar (down), that is m* = 0 if z + W < 1,
-// else ilogb(z + W) + 1 -- verified with the loop's own comparisons at 2^m* and 2^(m*-1)
-// (quick() is monotone in the probe, so the smaller probes agree with 2^(m*-1)); any probe
-// inside the window, or a rounding that breaks the verification, takes the loop.  Same
-// lo, hi and guard as the loop, ~20 instructions instead of ~20 per doubling.
-// Off by default (QR_BRACKET_FAST=0): it is exact (host replay check) but its extra live values
-// cost the hypothesis-parallel demapper an occupancy step (130 VGPRs -> 3 waves/SIMD).
-#ifndef QR_BRACKET_FAST
-#define QR_BRACKET_FAST 0
-#endif
-QR_HD int search_bracket_fast(const SearchCmp &cmp, double &lo, double &hi) {
-    const bool up = cmp.T > .5;
-    const double z = up ? cmp.ystar : -cmp.ystar;
-    const double x = z + cmp.W;
-    const int m = (x < 1.0) ? 0 : ilogb(x) + 1;
-    const double p = ldexp(1.0, m), q = (m > 0) ? ldexp(1.0, m - 1) : 0.0;
-    const int want = up ? 1 : -1;   // the stopping probe: F(2^m) > T (up) / F(-2^m) < T (down)
-    const bool ok = cmp.have && m >= 0 && m <= 1000 && cmp.quick(up ? p : -p) == want &&
-                    (m == 0 || cmp.quick(up ? q : -q) == -want);
-    if (!ok) return search_bracket(cmp, lo, hi);   // the one fallback (window probes, rounding)
-    lo = up ? q : -p;
-    hi = up ? p : -q;
-    return m;
-}
-
-// The reference's bracket + bisection (noisemapper.pyx:314-345) on a comparison oracle.
-QR_HD double search_replay(const SearchCmp &cmp) {
+// The reference's bracket + bisection (noisemapper.pyx:314-345) on a comparison oracle;
+// y_accuracy is the cpdef's optional argument (:310, default 1e-9).
+QR_HD double search_replay(const SearchCmp &cmp, double y_accuracy = 1e-9) {
     double lo, hi;
     int guard = search_bracket(cmp, lo, hi);
-    while ((hi - lo) > 1e-9) {
+    while ((hi - lo) > y_accuracy) {
         if (++guard > kSearchCap) { lo = hi = NAN; break; }
         const double mid = (hi + lo) / 2;
         int c = cmp.quick(mid);
@@ -273,7 +247,7 @@ QR_HD double search_replay(const SearchCmp &cmp) {
 // search_closed_finish applies the exact answer gt = (F_Y(end) > T).
 QR_HD bool search_closed_prepare(const SearchCmp &cmp, double &L, double &H, int &need) {
     double lo, hi;
-    const int guard = QR_BRACKET_FAST ? search_bracket_fast(cmp, lo, hi) : search_bracket(cmp, lo, hi);
+    const int guard = search_bracket(cmp, lo, hi);
     const double width = hi - lo;
     need = 0;
     if (!(width > 1e-9) || !(width <= 0x1p20) || !(cmp.W < 0x1p-31)) return false;
@@ -311,9 +285,18 @@ QR_HD double search_target(const DemapTables &t, double n_hat, int i) {
 }
 
 // Brute force: the reference algorithm verbatim.
-QR_HD double g_inv_search(const DemapTables &t, double n_hat, int i) {
+QR_HD double g_inv_search(const DemapTables &t, double n_hat, int i, double y_accuracy = 1e-9) {
     SearchCmp cmp{&t, search_target(t, n_hat, i), 0.0, 0.0, false};
-    return search_replay(cmp);
+    return search_replay(cmp, y_accuracy);
+}
+
+// noisemapper.pyx:264-275, the public cpdef F_Y: the UNIFORM mixture (sum of the M
+// component CDFs accumulated m = 0 first, then divided by the order), not the
+// probability-weighted _single_F_Y the search uses.
+QR_HD double public_F_Y(const DemapTables &t, double y) {
+    double res = 0.5 * (1 + cephes_erf((y - t.a[0]) / t.den));
+    for (int m = 1; m < t.M; ++m) res += 0.5 * (1 + cephes_erf((y - t.a[m]) / t.den));
+    return res / t.M;
 }
 
 // exp(x) with the LDS tables of fastmath.hpp (<= ~1 ulp, like ocml/glibc exp): x = k ln2/256 + r,

@@ -40,7 +40,29 @@ struct Stat {
     int64_t n = 0;
 };
 std::atomic<bool> g_prof{false};
-std::atomic<bool> g_prof_external{true};  // external event-record nodes accepted in captures
+// External event-record nodes accepted in stream captures: probed once, outside any capture of
+// the caller's, when profiling is switched on (-1 = not probed yet).  A failed external record
+// inside a live capture would invalidate that capture, so it is never attempted there.
+std::atomic<int> g_prof_external{-1};
+
+// A private relaxed-mode capture on a private stream holding one external event record.
+bool probe_external_records() {
+    hipStream_t s = nullptr;
+    hipEvent_t e = nullptr;
+    bool ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess && hipEventCreate(&e) == hipSuccess;
+    if (ok && hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed) == hipSuccess) {
+        ok = hipEventRecordWithFlags(e, s, hipEventRecordExternal) == hipSuccess;
+        hipGraph_t g = nullptr;
+        if (hipStreamEndCapture(s, &g) != hipSuccess) ok = false;
+        if (g) (void)hipGraphDestroy(g);
+    } else {
+        ok = false;
+    }
+    if (e) (void)hipEventDestroy(e);
+    if (s) (void)hipStreamDestroy(s);
+    (void)hipGetLastError();
+    return ok;
+}
 std::mutex g_prof_mu;
 std::vector<Pending> g_pending;
 std::map<std::string, Stat> g_stats;
@@ -78,16 +100,18 @@ ProfScope::ProfScope(std::string name, hipStream_t s) : name_(std::move(name)), 
     // times the launch of the latest replay when qr_profile_query drains it).
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     capture_ = s_ && hipStreamIsCapturing(s_, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
+    if (capture_ && g_prof_external.load() != 1) {  // no event-record nodes: captured launches go untimed
+        (void)hipEventDestroy(a_);
+        (void)hipEventDestroy(b_);
+        a_ = b_ = nullptr;
+        return;
+    }
     record(a_);
 }
 
 void ProfScope::record(hipEvent_t e) {
-    if (capture_ && g_prof_external.load()) {
-        if (hipEventRecordWithFlags(e, s_, hipEventRecordExternal) == hipSuccess) return;
-        (void)hipGetLastError();  // unsupported here: clear the sticky error, record plainly
-        g_prof_external.store(false);
-    }
-    (void)hipEventRecord(e, s_);
+    if (capture_) (void)hipEventRecordWithFlags(e, s_, hipEventRecordExternal);
+    else (void)hipEventRecord(e, s_);
 }
 
 ProfScope::~ProfScope() {
@@ -241,6 +265,7 @@ int qr_device_count(int32_t *count) {
 }
 
 int qr_profile_enable(int32_t on) {
+    if (on && qr::g_prof_external.load() < 0) qr::g_prof_external.store(qr::probe_external_records() ? 1 : 0);
     qr::g_prof.store(on != 0);
     return QR_OK;
 }

@@ -58,11 +58,10 @@ __host__ __device__ constexpr int pack_out_round(int D, int i) {
 // and for every t > 37.5 exp(-t) < 2^-54, so u = fl(1.0 + exp(-t)) == 1.0 and h == +0 in all
 // three modes: the same bits.
 enum { kClampNone = 0, kClampFull = 1, kClampFinite = 2 };
-template <int CL = kClampFull, int MJ = kPackMaxJobs, class TT = GlibcTables>
+template <int CL = kClampFull, class TT = GlibcTables>
 __device__ __forceinline__ void h_packed(const double *t, double *h, int nj, double *wb, const TT &T,
                                          const GlibcK &K) {
-    constexpr int kPackMaxJobs = MJ;  // (shadows the namespace constant: MJ arguments per lane)
-    constexpr int S = 64 * MJ + 64;
+    constexpr int S = kPackWaveDoubles;
     const uint32_t lane = __lane_id();
     uint32_t addr[kPackMaxJobs];  // byte address of the argument's slot
     uint32_t nN = 0;              // wave-uniform: near-1 arguments written so far
@@ -121,46 +120,31 @@ __device__ __forceinline__ void h_packed(const double *t, double *h, int nj, dou
 }
 
 // sgn(a) sgn(b) min(|a|, |b|) of the box-plus (decoder.pyx:41-45) with the magnitude from
-// v_min_f64 (QR_STRICT_FMIN, default): every operand here is the result of an fp64 add or
-// subtract, so the compiler knows it canonical and emits one v_min_f64 with |.| modifiers
-// instead of the compare + two selects.  Equal magnitudes have equal bits (+-0 included),
-// and a NaN operand makes both h arguments NaN, so the box-plus is NaN whatever min returns.
-#ifndef QR_STRICT_FMIN
-#define QR_STRICT_FMIN 1
-#endif
+// v_min_f64: every operand here is the result of an fp64 add or subtract, so the compiler
+// knows it canonical and emits one v_min_f64 with |.| modifiers instead of the compare + two
+// selects.  Equal magnitudes have equal bits (+-0 included), and a NaN operand makes both h
+// arguments NaN, so the box-plus is NaN whatever min returns.
 __device__ __forceinline__ double signed_min_packed(double a, double b) {
-#if QR_STRICT_FMIN
     const double mn = __builtin_fmin(__builtin_fabs(a), __builtin_fabs(b));
     return g_make(g_bfi(0x7FFFFFFFu, g_hi(mn), g_hi(a) ^ g_hi(b)), g_lo(mn));
-#else
-    return signed_min(a, b);
-#endif
 }
 
 // decoder.pyx:322-369 for one check of degree D (>= 2): out[i] = c2v of edge i before
 // the syndrome sign.  The same box-plus (operands and box_plus_strict's operation order)
 // as check_exact<kStrict>, evaluated round by round.
-// NC checks of degree D side by side (the same rounds; their log arguments packed together:
-// one partly filled slice per kind and round for all NC checks instead of one per check).
-template <int D, int CL = kClampFull, int NC = 1, class TT = GlibcTables>
-__device__ __forceinline__ void check_strict_packed_n(const double (&m)[NC][D], double (&out)[NC][D], double *wb,
-                                                      const TT &T, const GlibcK &K) {
+template <int D, int CL = kClampFull, class TT = GlibcTables>
+__device__ __forceinline__ void check_strict_packed(const double (&m)[D], double (&out)[D], double *wb, const TT &T,
+                                                    const GlibcK &K) {
     if constexpr (D == 2) {
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            out[c][0] = m[c][1];
-            out[c][1] = m[c][0];
-        }
+        out[0] = m[1];
+        out[1] = m[0];
     } else {
-        double F[NC][D], Bv[NC][D];
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            F[c][0] = m[c][0];
-            Bv[c][D - 1] = m[c][D - 1];
-        }
+        double F[D], Bv[D];
+        F[0] = m[0];
+        Bv[D - 1] = m[D - 1];
 #pragma unroll
         for (int r = 1; r <= D - 2; ++r) {
-            // the round's box-plus: kind 0 = F_r, 1 = B_{D-1-r}, 2 = O_i (the same list for every check)
+            // the round's box-plus: kind 0 = F_r, 1 = B_{D-1-r}, 2 = O_i
             int kind[4], idx[4];
             int k = 0;
             kind[k] = 0, idx[k] = r, ++k;
@@ -169,44 +153,29 @@ __device__ __forceinline__ void check_strict_packed_n(const double (&m)[NC][D], 
             for (int i = 1; i <= D - 2; ++i)
                 if (pack_out_round(D, i) == r) kind[k] = 2, idx[k] = i, ++k;
             // box_plus_strict_t: (sm + h(|a + b|)) - h(|a - b|)
-            double t[8 * NC], h[8 * NC], sm[4 * NC];
+            double t[8], h[8], sm[4];
 #pragma unroll
-            for (int c = 0; c < NC; ++c) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    if (q >= k) break;
-                    const double a = kind[q] == 0 ? F[c][r - 1] : kind[q] == 1 ? Bv[c][D - r] : F[c][idx[q] - 1];
-                    const double b = kind[q] == 0 ? m[c][r] : kind[q] == 1 ? m[c][D - 1 - r] : Bv[c][idx[q] + 1];
-                    sm[4 * c + q] = signed_min_packed(a, b);
-                    t[2 * (k * c + q)] = a + b;
-                    t[2 * (k * c + q) + 1] = a - b;
-                }
+            for (int q = 0; q < 4; ++q) {
+                if (q >= k) break;
+                const double a = kind[q] == 0 ? F[r - 1] : kind[q] == 1 ? Bv[D - r] : F[idx[q] - 1];
+                const double b = kind[q] == 0 ? m[r] : kind[q] == 1 ? m[D - 1 - r] : Bv[idx[q] + 1];
+                sm[q] = signed_min_packed(a, b);
+                t[2 * q] = a + b;
+                t[2 * q + 1] = a - b;
             }
-            h_packed<CL, 8 * NC>(t, h, 2 * k * NC, wb, T, K);
+            h_packed<CL>(t, h, 2 * k, wb, T, K);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    if (q >= k) break;
-                    const double v = (sm[4 * c + q] + h[2 * (k * c + q)]) - h[2 * (k * c + q) + 1];
-                    if (kind[q] == 0) F[c][idx[q]] = v;
-                    else if (kind[q] == 1) Bv[c][idx[q]] = v;
-                    else out[c][idx[q]] = v;
-                }
+            for (int q = 0; q < 4; ++q) {
+                if (q >= k) break;
+                const double v = (sm[q] + h[2 * q]) - h[2 * q + 1];
+                if (kind[q] == 0) F[idx[q]] = v;
+                else if (kind[q] == 1) Bv[idx[q]] = v;
+                else out[idx[q]] = v;
             }
         }
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            out[c][0] = Bv[c][1];
-            out[c][D - 1] = F[c][D - 2];
-        }
+        out[0] = Bv[1];
+        out[D - 1] = F[D - 2];
     }
-}
-template <int D, int CL = kClampFull, class TT = GlibcTables>
-__device__ __forceinline__ void check_strict_packed(const double (&m)[D], double (&out)[D], double *wb,
-                                                    const TT &T, const GlibcK &K) {
-    check_strict_packed_n<D, CL, 1>(reinterpret_cast<const double(&)[1][D]>(m), reinterpret_cast<double(&)[1][D]>(out),
-                                    wb, T, K);
 }
 
 }  // namespace qr

@@ -51,6 +51,8 @@ SIGNATURES = {
     "qr_demap_tables": [vp, vp, vp],
     "qr_demap_batch_device": [vp, i32, i32, i64, vp, vp, f64, vp, vp],
     "qr_demap_host": [vp, i64, vp, vp, vp],
+    "qr_g_inv_search_host": [vp, i64, vp, vp, f64, vp],
+    "qr_F_Y_host": [vp, i64, vp, vp],
     "qr_bob_map_device": [vp, i32, i32, i64, vp, vp, vp, vp, vp],
     "qr_map_noise_device": [vp, i32, i32, i64, vp, vp, vp, vp],
     "qr_syndrome_device": [vp, i32, i32, vp, vp, vp],

@@ -137,6 +137,12 @@ def all_reduce_max(t):
     return _all_reduce(t, dist.ReduceOp.MAX)
 
 
+def all_reduce_min(t):
+    import torch.distributed as dist
+
+    return _all_reduce(t, dist.ReduceOp.MIN)
+
+
 def barrier():
     import torch.distributed as dist
 
@@ -152,8 +158,9 @@ def finalize():
 
 
 def early_stop(counters, ferr_count_min: int, simulation_loops: int) -> bool:
-    """reconciliation.pyx:159-161 at batch granularity: frame_errors >= ferr_count_min
-    and (frames processed - 1) > simulation_loops / 20."""
+    """reconciliation.pyx:159-161 after the last frame counted: frame_errors >= ferr_count_min
+    and wordcount = (frames processed - 1) > simulation_loops / 20 (qamr.sim then locates the
+    first frame at which it held)."""
     frames = int(counters[4])
     return int(counters[1]) >= ferr_count_min and (frames - 1) > simulation_loops / 20
 

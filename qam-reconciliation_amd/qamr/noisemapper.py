@@ -170,6 +170,46 @@ class NoiseMapper:
         """noisemapper.pyx:362-370"""
         return self.constellation[np.asarray(index, np.int64)]
 
+    # ------------------------------------- CDF and its inverse (GPU, scalar API)
+    def F_Y(self, y):
+        """noisemapper.pyx:264-275: the uniformly weighted mixture CDF at every y."""
+        y = np.asarray(y)
+        if y.dtype != np.float64:
+            raise ValueError(f"Buffer dtype mismatch, expected 'double' but got '{y.dtype}'")
+        y = np.ascontiguousarray(y.ravel())
+        out = np.empty(y.size, np.float64)
+        if y.size:
+            check(_lib.load().qr_F_Y_host(self._h, y.size, ptr(y), ptr(out)), "F_Y")
+        return out
+
+    def g(self, y, i):
+        """noisemapper.pyx:289-292: the transformed noise of sample y in decision region i."""
+        return float(self.map_noise(np.array([float(y)]), np.array([int(i)], np.int64))[0])
+
+    def g_inv_search(self, n_hat, i, y_accuracy=1e-9):
+        """noisemapper.pyx:310-345: y with F_Y(y) = the target of (n_hat, i), by doubling
+        bracket + bisection to width <= y_accuracy."""
+        return float(self.demap_noise_search(np.array([float(n_hat)]), np.array([int(i)], np.int64),
+                                             y_accuracy)[0])
+
+    def demap_noise_search(self, n_hat, symb, y_accuracy=1e-9):
+        """noisemapper.pyx:407-419: g_inv_search over arrays."""
+        n_hat = np.asarray(n_hat)
+        symb = np.asarray(symb)
+        if n_hat.dtype != np.float64:
+            raise ValueError(f"Buffer dtype mismatch, expected 'double' but got '{n_hat.dtype}'")
+        if symb.dtype != np.int64:
+            raise ValueError(f"Buffer dtype mismatch, expected 'long' but got '{symb.dtype}'")
+        if n_hat.size != symb.size:
+            raise ValueError("Sizes do not match")
+        n_hat = np.ascontiguousarray(n_hat.ravel())
+        symb = np.ascontiguousarray(symb.ravel())
+        out = np.empty(n_hat.size, np.float64)
+        if n_hat.size:
+            check(_lib.load().qr_g_inv_search_host(self._h, n_hat.size, ptr(n_hat), ptr(symb), float(y_accuracy),
+                                                   ptr(out)), "g_inv_search")
+        return out
+
     # ------------------------------------------------------- hot path (GPU)
     def demap_lappr_array(self, n, j):
         """noisemapper.pyx:544-559: LAPPRs [S*bps], out[s*bps + k] = Gray bit k of symbol s."""

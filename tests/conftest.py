@@ -8,6 +8,7 @@ ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 sys.path.insert(0, os.path.join(ROOT, "qam-reconciliation_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, GOLDEN)
 
 
 def pytest_configure(config):

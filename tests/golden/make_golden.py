@@ -308,9 +308,46 @@ def gen_llr_sources():
     np.savez_compressed(os.path.join(HERE, "llr_sources.npz"), **out)
 
 
+from make_golden_cases import NOISE_SEARCH_ACC, NOISE_SEARCH_CASES  # noqa: E402
+
+
+def gen_noise_search():
+    """The cpdef surface of NoiseMapper around the search (noisemapper.pyx:264-345, 407-419):
+    F_Y on a y grid, g(y, i), and g_inv_search(n_hat, i, y_accuracy) for every decision
+    region, both sign configurations, edge n_hat (0, 1, 1/2, subnormal, 1 - 2^-53 ...) and
+    y_accuracy in {1e-6, 1e-9, 1e-12}."""
+    out = {}
+    for c, (bps, snr, probs) in enumerate(NOISE_SEARCH_CASES):
+        pa = PAMAlphabet(bps, 2.0, None if probs is None else np.array(probs))
+        nv = noise_var(pa, snr)
+        rng = np.random.default_rng(500 + c)
+        k = f"c{c}"
+        out[f"{k}_noise_var"] = nv
+        M = pa.order
+        edge = np.array([0.0, 1.0, 0.5, 5e-324, 1e-300, 1e-17, 1e-9, 1 - 2 ** -53, 0.25, 0.999999])
+        nh = np.concatenate([edge, rng.uniform(0, 1, 14)])
+        ii = np.arange(M, dtype=np.int64)
+        # y grid through every region and far into both tails
+        y = np.concatenate([np.linspace(pa.constellation[0] * 1.6, pa.constellation[-1] * 1.6, 41),
+                            rng.normal(0, 2 * M, 24), np.array([0.0, -0.0, 1e3, -1e3, 40.0, -40.0])])
+        out[f"{k}_y"] = y
+        gi = rng.integers(0, M, y.size).astype(np.int64)
+        out[f"{k}_gi"] = gi
+        for cfgname, cfg in (("base", None), ("alt", alternating(M))):
+            nm = NoiseMapper(pa, nv, cfg) if cfg is not None else NoiseMapper(pa, nv)
+            out[f"{k}_{cfgname}_F_Y"] = np.asarray(nm.F_Y(y.copy()))
+            out[f"{k}_{cfgname}_g"] = np.array([nm.g(float(yy), int(i)) for yy, i in zip(y, gi)])
+            for a_i, acc in enumerate(NOISE_SEARCH_ACC):
+                res = np.array([[nm.g_inv_search(float(n), int(i), acc) for n in nh] for i in ii])
+                out[f"{k}_{cfgname}_ginv_a{a_i}"] = res
+            out[f"{k}_{cfgname}_dns"] = np.asarray(nm.demap_noise_search(nh.copy(), np.full(nh.size, M // 2 - 1 if M > 1 else 0, np.int64)))
+        out[f"{k}_nhat"] = nh
+    np.savez_compressed(os.path.join(HERE, "noise_search.npz"), **out)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["hamming", "node_rules", "reg1008", "demap", "pam16_nan", "llr_sources", "dvbs2",
-                             "dvbs2_16pam"]
+                             "dvbs2_16pam", "noise_search"]
     for w in which:
         t = time.time()
         print(f"[golden] {w}", flush=True)

@@ -11,8 +11,7 @@ import pytest
 from conftest import ROOT
 
 
-@pytest.mark.parametrize("flags", [[], ["-DQR_BRACKET_FAST=1"]])
-def test_fast_search_bit_identical(tmp_path, flags):
+def test_fast_search_bit_identical(tmp_path):
     src = os.path.join(ROOT, "tests", "native", "replay_check.cpp")
     exe = str(tmp_path / "replay_check")
     csrc = os.path.join(ROOT, "qam-reconciliation_amd", "csrc")
@@ -21,7 +20,7 @@ def test_fast_search_bit_identical(tmp_path, flags):
     subprocess.run([sys.executable, os.path.join(csrc, "gen_glibc_tables.py"), str(tmp_path / "glibc_tables.inc")],
                    check=True)
     cc = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "-ffp-contract=off", "-std=c++17",
-                         "-I" + csrc, "-I" + str(tmp_path), *flags, "-o", exe, src], capture_output=True, text=True)
+                         "-I" + csrc, "-I" + str(tmp_path), "-o", exe, src], capture_output=True, text=True)
     assert cc.returncode == 0, cc.stderr[-2000:]
     run = subprocess.run([exe, "120000"], capture_output=True, text=True, timeout=300)
     print(run.stdout)

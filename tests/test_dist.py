@@ -208,3 +208,105 @@ def test_bench_rank_body_under_rccl_capability(monkeypatch, capsys):
     assert len(seen) >= 2 and all(ok for _, ok in seen)  # timed-region max + counter sum
     B = out["config"]["batch_per_gpu"]
     assert out["counters"] == [2 * 10, 2 * 1, 2 * (B - 1), 2 * 7 * (B - 1), 2 * B]
+
+
+# ------------------------------------------------ configs[4]'s rank count (8 ranks, CPU)
+def _check_world8(out):
+    assert out["n_gpus"] == 8
+    B = out["config"]["batch_per_gpu"]
+    assert out["config"]["global_batch"] == 8 * B == 32768      # configs[4]: 8 x 4096 frames
+    assert out["config"]["parallelism"] == "dp8" and out["config"]["backend"] == "gloo"
+    # StubWork rank r contributes [10(r+1), r+1, B-r-1, 7(B-r-1), B]
+    assert out["counters"] == [10 * 36, 36, 8 * B - 36, 7 * (8 * B - 36), 8 * B]
+    assert out["config"]["rank_devices"] == list(range(8))     # rank r bound LOCAL_RANK r
+
+
+def test_bench_gpus8_self_launch():
+    """`bench.py --gpus 8` (configs[4]'s launch at its real rank count) starting its 8 ranks
+    itself: world size, global batch 32768, summed counters, rank r bound to GPU r."""
+    _check_world8(_bench_line([BENCH, "--gpus", "8", "--steps", "2", "--warmup", "1", "--batch", "4096"]))
+
+
+def test_bench_gpus8_torchrun():
+    """The driver's N=8 launch: torch.distributed.run --nproc-per-node 8 bench.py --gpus 8."""
+    _check_world8(_bench_line(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                               BENCH, "--gpus", "8", "--steps", "2", "--warmup", "1", "--batch", "4096"]))
+
+
+# synthetic per-frame results of global frame g (bit errors, success, iterations)
+def _frame_synth(g):
+    ferr = (g * 2654435761 % 97 + 1) if (g * 7919) % 5 == 0 else 0
+    return ferr, int(g % 3 != 0), 1 + g % 29
+
+
+FRAME_CASES = [  # (batch per rank, simulation_loops, ferr_count_min)
+    (16, 1000, 30),      # stops inside a later batch
+    (5, 37, 2),          # one ragged batch (37 < 8 x 5)
+    (3, 100, 10 ** 6),   # never stops: ragged last batch
+    (1, 20, 0),          # ferr_count_min 0: stops at the first wordcount > loops / 20
+    (4, 6, 1),           # fewer frames than ranks: ranks 6, 7 hold none
+    (7, 500, 12),
+]
+
+
+def _frames_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "qam-reconciliation_amd"))
+    from qamr import dist
+    from qamr.sim import run_frames, shard_counters
+
+    dist.init("gloo")
+    res = []
+    for batch, loops, fmin in FRAME_CASES:
+        def fn(bidx, start, B, batch=batch):
+            g0 = bidx * batch * world + start          # every batch before the last is full
+            rows = [_frame_synth(g) for g in range(g0, g0 + B)]
+            ferr = torch.tensor([r[0] for r in rows], dtype=torch.int32)
+            succ = torch.tensor([r[1] for r in rows], dtype=torch.uint8)
+            its = torch.tensor([r[2] for r in rows], dtype=torch.int32)
+            return ferr, succ, its, shard_counters(ferr, succ, its, B)
+        res.append(run_frames(fn, batch, loops, fmin))
+    dist.barrier()
+    dist.finalize()
+    q.put((rank, res))
+
+
+def _sequential(loops, fmin):
+    """sims/reconciliation.pyx:127-168 over the same frames, one at a time."""
+    be = fe = su = it = 0
+    w = -1
+    for w in range(loops):
+        e, s, i = _frame_synth(w)
+        if s:
+            it += i
+            su += 1
+        if e:
+            fe += 1
+            be += e
+        if fe >= fmin and w > loops / 20:
+            break
+    return [be, fe, su, it, w + 1]
+
+
+def test_run_frames_world8_exact_early_stop():
+    """qamr.sim.run_frames (Simulator.run_snr's shard / reduce / early-stop loop) at world size 8
+    over gloo with stub frames: every rank returns the counters of the reference's sequential
+    loop, cut at the same frame (per-frame rule, not batch granularity)."""
+    world, port = 8, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_frames_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for c, (batch, loops, fmin) in enumerate(FRAME_CASES):
+        exp = _sequential(loops, fmin)
+        for r in range(world):
+            assert res[r][c] == exp, (c, r, res[r][c], exp)

@@ -268,7 +268,7 @@ def test_decode_device_graph_capture(gpu):
     S = torch.from_numpy(synd.T.copy()).cuda()
     saved = _lib.tune_get("split")
     try:
-        for split in (4, 3, 2, 1):
+        for split in (3, 2, 1):
             _lib.tune_set("split", split)
             ref = [x.clone() for x in dec.decode_device(L, S, B, 30)]  # eager (also allocates)
             fin = torch.full_like(L, np.nan)

@@ -229,3 +229,76 @@ def test_hypothesis_parallel_demap_equals_per_symbol(gpu, bps, snr):
         for f in (0, 63, 64, B - 1):
             ref = onm.demap_lappr_array(n[2:, f].copy(), x[2:, f].copy()) * 0.5
             assert_bit_exact(a[2 * bps:, f], ref)
+
+
+# --------------------------------------- F_Y / g / g_inv_search surface (noisemapper.pyx:264-419)
+def _case_nm(c):
+    import qamr
+    import make_golden_cases as MC
+    bps, _, probs = MC.NOISE_SEARCH_CASES[c]
+    return bps, (None if probs is None else np.array(probs))
+
+
+@pytest.mark.parametrize("c", range(7))
+def test_noise_search_surface_vs_reference(gpu, c):
+    """NoiseMapper.F_Y / g / g_inv_search(n_hat, i, y_accuracy) / demap_noise_search through
+    libqamr (qr_F_Y_host, qr_g_inv_search_host, qr_map_noise_device) against the reference's
+    own outputs: every region, both sign configurations, edge n_hat, y_accuracy 1e-6 / 1e-9 /
+    1e-12 (the fast certified search at 1e-9, the verbatim loops otherwise)."""
+    import qamr
+    import make_golden_cases as MC
+    g = golden("noise_search.npz")
+    bps, probs = _case_nm(c)
+    k = f"c{c}"
+    M = 1 << bps
+    pa = qamr.PAMAlphabet(bps, 2.0, probs)
+    for cfgname in ("base", "alt"):
+        cfg = None if cfgname == "base" else MC.alternating(M)
+        nm = qamr.NoiseMapper(pa, float(g[f"{k}_noise_var"]), cfg)
+        assert_bit_exact(nm.F_Y(g[f"{k}_y"]), g[f"{k}_{cfgname}_F_Y"])
+        assert_bit_exact([nm.g(y, i) for y, i in zip(g[f"{k}_y"], g[f"{k}_gi"])], g[f"{k}_{cfgname}_g"])
+        nh = g[f"{k}_nhat"]
+        for a_i, acc in enumerate(MC.NOISE_SEARCH_ACC):
+            ref = g[f"{k}_{cfgname}_ginv_a{a_i}"]
+            got = nm.demap_noise_search(np.tile(nh, M), np.repeat(np.arange(M, dtype=np.int64), nh.size), acc)
+            assert_bit_exact(got.reshape(M, nh.size), ref)
+            # the scalar cpdef on a few points
+            for i in (0, M - 1):
+                assert_bit_exact([nm.g_inv_search(nh[3], i, acc)], [ref[i, 3]])
+        sym = np.full(nh.size, M // 2 - 1 if M > 1 else 0, np.int64)
+        assert_bit_exact(nm.demap_noise_search(nh, sym), g[f"{k}_{cfgname}_dns"])
+
+
+def test_noise_search_random_vs_oracle_and_errors(gpu):
+    """Random (n_hat, i) at other accuracies (incl. an exact power of two, where the loop stops
+    at width == y_accuracy), fast vs brute search identical, the oracle as checker; out-of-range
+    i -> NaN; size / dtype mismatch -> ValueError (noisemapper.pyx:410-411)."""
+    import qamr
+    from qamr import _lib
+    rng = np.random.default_rng(17)
+    for bps, nv in ((2, 0.35), (3, 0.8), (4, 0.05)):
+        M = 1 << bps
+        cfg = rng.integers(0, 2, M).astype(np.uint8)
+        nm = _nm(bps, nv, cfg)
+        onm = O.OracleNoiseMapper(bps, 2.0, nv, cfg)
+        n = rng.uniform(0, 1, 256)
+        i = rng.integers(0, M, 256).astype(np.int64)
+        for acc in (1e-3, 2.0 ** -20, 1e-9, 3e-11):
+            got = nm.demap_noise_search(n, i, acc)
+            assert_bit_exact(got, [onm.g_inv_search(a, b, acc) for a, b in zip(n, i)])
+        saved = _lib.tune_get("demap_fast")
+        try:
+            _lib.tune_set("demap_fast", 0)
+            brute = nm.demap_noise_search(n, i)
+        finally:
+            _lib.tune_set("demap_fast", saved)
+        assert_bit_exact(nm.demap_noise_search(n, i), brute)
+    nm = _nm(2, 1.0)
+    assert np.isnan(nm.demap_noise_search(np.array([0.5, 0.5]), np.array([-1, 4], np.int64))).all()
+    with pytest.raises(ValueError):
+        nm.demap_noise_search(np.zeros(3), np.zeros(2, np.int64))
+    with pytest.raises(ValueError):
+        nm.demap_noise_search(np.zeros(3, np.float32), np.zeros(3, np.int64))
+    with pytest.raises(ValueError):
+        nm.F_Y(np.zeros(3, np.int64))
+    assert nm.F_Y(np.zeros(0)).size == 0

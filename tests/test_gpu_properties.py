@@ -72,14 +72,12 @@ def _dvbs2_batch(B, snr_db, seed=0):
 
 
 TUNINGS = [dict(split=1), dict(split=2, check_per=1), dict(check_ft=64, check_per=3, var_ft=128, var_per=1),
-           dict(nt=0), dict(split=1, check_ft=128, var_per=16), dict(split=3), dict(split=3, lds_pad_kb=0, nt=0),
-           dict(split=2), dict(compact=0), dict(split=1, compact=0), dict(split=2, compact=0), dict(side=0),
-           dict(side=0, compact=0), dict(split=4), dict(split=4, compact=0), dict(min_blocks=0),
-           dict(min_blocks=4096, split=1), dict(split_min_blocks=4096), dict(split_min_blocks=0, min_blocks=0),
-           dict(var_pace=0), dict(var_pace=1), dict(var_pace=3, var_per=1, compact=0), dict(var_pace=4096),
-           dict(split=5), dict(split=5, compact=0, side=0), dict(split=5, var_pace=0),
-           dict(check_tail=0), dict(check_tail=16), dict(check_tail=3, check_per=7, compact=0),
-           dict(check_tail=2, split=1)]
+           dict(nt=0), dict(split=1, check_ft=128, var_per=16), dict(split=3, lds_pad_kb=0, nt=0),
+           dict(split=2), dict(compact=0), dict(split=1, compact=0), dict(split=2, compact=0),
+           dict(side=0, compact=0), dict(min_blocks=0), dict(min_blocks=4096, split=1),
+           dict(split_min_blocks=4096), dict(split_min_blocks=0, min_blocks=0),
+           dict(var_pace=0), dict(var_pace=3, var_per=1, compact=0), dict(var_pace=4096),
+           dict(check_tail=0), dict(check_tail=3, check_per=7, compact=0), dict(check_tail=2, split=1)]
 
 
 def test_schedule_and_tuning_invariance(gpu):

@@ -106,3 +106,58 @@ def test_run_snr_and_cli(gpu, tmp_path):
     assert len(rows) == 2 and rows[1][2] <= rows[0][2]  # FER decreases with SNR
     lines = open(out).read().splitlines()
     assert lines[0] == ",EsN0dB,ber,fer,iters" and len(lines) == 3
+
+
+def _reference_loop(frames, K, simulation_loops, ferr_count_min):
+    """sims/reconciliation.pyx:127-168 verbatim over per-frame (success, iterations, final,
+    word) in frame order: the counters and the stop at the first frame where the rule holds."""
+    err_count = frame_error_count = decoding_iterations = successful_decoding = 0
+    wordcount = -1
+    for wordcount in range(simulation_loops):
+        success, iterations, final, word = frames[wordcount]
+        if success:
+            decoding_iterations += iterations
+            successful_decoding += 1
+        new_errors = O.count_errors_from_lappr(final[:K], word[:K])
+        if new_errors:
+            frame_error_count += 1
+            err_count += new_errors
+        if frame_error_count >= ferr_count_min and wordcount > simulation_loops / 20:
+            break
+    wordcount += 1
+    return (err_count / (wordcount * K), frame_error_count / wordcount,
+            0 if successful_decoding == 0 else decoding_iterations / successful_decoding), wordcount
+
+
+@pytest.mark.parametrize("loops,ferr_min,batch,snr", [(400, 7, 64, 1.8), (300, 40, 48, 2.2), (120, 1000, 64, 1.8)])
+def test_run_snr_exact_early_stop(gpu, loops, ferr_min, batch, snr):
+    """Simulator.run_snr stops at the reference's frame, not at a batch boundary: the GPU's own
+    frames (captured through the hook) re-decoded one by one by the oracle and run through the
+    reference's sequential loop give the same (snr, ber, fer, iters) tuple."""
+    import torch
+    import qamr
+    from qamr import codes
+    from qamr.sim import Simulator
+
+    vid, cid = codes.regular_code(1008)
+    dec = qamr.Decoder(vid, cid)
+    orc = O.OracleCode(vid, cid)
+    sim = Simulator(dec, 2, "softening", max_iterations=30, batch=batch)
+    seen = []
+
+    def hook(bidx, lappr, synd, word, B):
+        torch.cuda.synchronize()
+        seen.append((bidx, lappr[:, :B].cpu().numpy().T.copy(), synd[:, :B].cpu().numpy().T.copy(),
+                     word[:, :B].cpu().numpy().T.copy()))
+
+    got = sim.run_snr(snr, loops, ferr_min, seed=4, hook=hook)
+    frames = []
+    for bidx, L, Sy, W in sorted(seen, key=lambda t: t[0]):
+        s, i, f = orc.decode_batch(L, Sy, 30)
+        frames += [(int(s[k]), int(i[k]), f[k], W[k]) for k in range(L.shape[0])]
+    ref, stop = _reference_loop(frames, sim.K, loops, ferr_min)
+    assert got == (snr,) + ref, (got, ref, stop)
+    if ferr_min < 1000:
+        assert stop < loops and stop % batch != 0, stop   # the stop fell inside a batch
+    else:
+        assert stop == loops
