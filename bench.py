@@ -54,6 +54,7 @@ from qamr import dist  # noqa: E402  (pure Python; touches no GPU)
 
 METRIC = "decoded frames/sec @ N=64800, 50 BP iters; achieved HBM GB/s vs roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+GUIDE_COPY_GBS = 6290.0  # float4 streaming copy measured on MI355X (MI355X_MICROARCH.md: 79 % of spec)
 # fp64 VALU: 78.6 TFLOP/s spec = 1024 SIMDs x 2.4 GHz x 16 fp64 FMA lanes: a wave64 fp64
 # instruction occupies its SIMD 4 cycles, 32-bit VALU 2 cycles (MI355X_MICROARCH.md).
 SIMDS, CLOCK_HZ = 1024, 2.4e9
@@ -427,7 +428,8 @@ def roofline(args, w, kstats, dev, world=1):
             "frac": round(frac, 4), "traffic": traffic, "kernel": kname,
             "bytes_per_launch": int(bytes_launch), "avg_launch_us": round(avg_s * 1e6, 1),
             "launches": kstats[kkey]["launches"],
-            "measured_copy_GBps": round(copy_gbps, 1), "frac_of_copy": round(ach / copy_gbps, 4), "valu": valu}
+            "measured_copy_GBps": round(copy_gbps, 1), "frac_of_copy": round(ach / copy_gbps, 4),
+            "guide_copy_GBps": GUIDE_COPY_GBS, "frac_of_guide_copy": round(ach / GUIDE_COPY_GBS, 4), "valu": valu}
 
 
 def secondary(args, rank, local):

@@ -213,7 +213,7 @@ QR_API int qr_to_frame_innermost_u8(int32_t B, int32_t ld, int64_t n, const uint
 QR_API int qr_to_frame_innermost_i64(int32_t B, int32_t ld, int64_t n, const int64_t *d_src, int64_t *d_dst, void *stream);
 
 /* ------------------------------------------------------------ measurement */
-/* Streaming device copy (16 B per lane, grid-stride): the practical HBM ceiling
+/* Streaming device copy (4 x 16 B per lane in flight, grid-stride): the practical HBM ceiling
  * the decoder's roofline is related to in bench.py. bytes % 16 == 0,
  * 16-B aligned pointers.  Not a reference interface. */
 QR_API int qr_stream_copy(const void *d_src, void *d_dst, int64_t bytes, void *stream);

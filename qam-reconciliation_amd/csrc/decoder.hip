@@ -153,6 +153,15 @@ struct CheckArgs {
     // workgroup's time.  nmain = 0: the plain 2-D grid (nbx x frame tiles).
     unsigned nmain;
     int per_t;
+    // Work queue (knob check_queue; k_check main sweeps only): a grid of about one resident
+    // wave of workgroups dequeues items (frame tile, check block) from *queue (zeroed per launch)
+    // instead of one workgroup per item.  The tiles swept are the live ones (ceil(*acount / ft)
+    // with compaction, else ntiles); the last live tile is cut into per_t-check items (the short
+    // tail), the others into g.per-check items.  Without compaction the grid would be ntiles x
+    // nbx workgroups however few frames still run; with it, no workgroup is dispatched for
+    // nothing and no launch ends in a partly filled wave of workgroups.
+    unsigned *queue;
+    unsigned ntiles, nbx_t;
 };
 
 // One variable sweep over the frame columns [f_off, f_off + ny*ft).
@@ -420,10 +429,48 @@ struct ClkScope {
     }
 };
 #endif
+// The work-queue sweep (CheckArgs::queue): item k of the live tiles 0..L-1 is check block
+// k % nbx of tile k / nbx with g.per checks per thread, and the last live tile's items come
+// last with per_t.  One lane dequeues, the workgroup follows (two barriers per item).
+template <int D, int MODE, bool NT, int AR, bool FIN>
+__device__ __forceinline__ void check_queue(const CheckArgs &a, const typename Arith<AR>::Tab &tab, double *hb) {
+    __shared__ unsigned s_item;
+    unsigned L = a.ntiles;
+    if (a.acount) {
+        const unsigned cnt = (unsigned)max(0, sld(a.acount));
+        L = min(L, (cnt + (1u << a.g.lft) - 1) >> a.g.lft);
+    }
+    if (L == 0) return;  // grid-uniform
+    const unsigned nfull = (L - 1) * a.nbx, nitems = nfull + a.nbx_t;
+    for (;;) {
+        if (threadIdx.x == 0) s_item = atomicAdd(a.queue, 1u);
+        __syncthreads();
+        const unsigned k = s_item;
+        __syncthreads();  // s_item is rewritten by the next dequeue
+        if (k >= nitems) return;  // block-uniform
+        if (k < nfull) check_block<D, MODE, NT, AR, FIN>(a, k % a.nbx, k / a.nbx, a.g.per, tab, hb);
+        else check_block<D, MODE, NT, AR, FIN>(a, k - nfull, L - 1, a.per_t, tab, hb);
+    }
+}
+
 template <int D, int MODE, bool NT, int AR>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) k_check(CheckArgs a) {
     __shared__ typename Arith<AR>::Tab tab;
     __shared__ double hb[PackLds<AR>::doubles];
+    if (MODE != kParityOnly && a.queue) {
+#if QR_EXPERIMENT_CLOCK
+        ClkScope clk(D == 7 && MODE == kNormal && AR == kStrict);
+#endif
+        stage_tables<AR>(&tab, a);
+        if constexpr (kPacked<AR, D>) {
+            if (a.finite && sld(a.finite)) {  // kernel-uniform: one of the two bodies runs
+                check_queue<D, MODE, NT, AR, true>(a, tab, hb);
+                return;
+            }
+        }
+        check_queue<D, MODE, NT, AR, false>(a, tab, hb);
+        return;
+    }
     unsigned bx = blockIdx.x, by = blockIdx.y;
     int per = a.g.per;
     if (a.nmain) {  // short-tail 1-D grid (block-uniform)
@@ -462,6 +509,109 @@ __global__ void __launch_bounds__(256) k_var(VarArgs a) {
     }
     if (!frames_block_live(a.acount, blockIdx.y, a.g.lft)) return;
     var_block<INIT, NT>(a, blockIdx.x, blockIdx.y);
+}
+
+// ---------------------------------------------------------------------------------------
+// Small codes (configs[1], reg-(3,6) N=1008): ONE launch per iteration.  A sweep of such a
+// code is a few microseconds of chip work, so the three launches of the flat schedule
+// (check, status, variable) are dominated by dispatch and drain.  Here the check sweep
+// computes the posteriors it needs itself, from the previous iteration's messages:
+//   post(t-1)[v] = lappr[v] + c2v(t-1)[e_0] + c2v(t-1)[e_1] + ...   (ascending edge id,
+//                  decoder.pyx:292-293 -- the same additions, so the same bits)
+// and the check whose edge is v's first edge stores it (the decoder's output), so no
+// variable sweep is needed.  The messages are double-buffered by iteration parity (a check
+// of iteration t reads c2v(t-1) of edges other checks are rewriting).  Launch P(t):
+//   * status of iteration t-2 (t >= 3): frames whose post(t-2) satisfied the syndrome stop
+//     with (1, t-2); the check of index 0 of each frame writes it, every lane derives the
+//     same running flag act = active && unsat(t-2) (so the write races benignly);
+//   * post(t-1) on the fly, its parity (unsat(t-1), t >= 2), c2v(t) (t <= max_it).
+// Per frame the order is the reference's: check(t) -> status(t-1) -> var(t) -> check(t+1);
+// P(max_it + 1) is the final parity sweep.  Used for single-degree-class codes with D <= 10
+// when the split schedules do not pay (knob fused_iter).
+struct IterArgs {
+    const int32_t *checks;
+    int64_t n_checks;
+    const int32_t *chk_ptr, *chk_edge, *chk_var, *var_ptr, *var_edge;
+    const double *lappr;
+    double *post;
+    const double *c2v_in;  // c2v(t-1), or null at t = 1 (all messages 0)
+    double *c2v_out;       // c2v(t), or null in the final parity sweep
+    const uint8_t *synd;
+    uint8_t *active, *success;
+    int32_t *iters;
+    const uint8_t *unsat_s;  // row t-2 (status to apply), or null
+    uint8_t *unsat_p;        // row t-1 (parity of post(t-1)), or null at t = 1
+    int32_t status_iter;     // t - 2
+    int ld;
+    Geom g;
+    unsigned nbx;
+    const GlibcTables *gglibc;
+    const int32_t *finite;
+};
+
+template <int D, bool NT, bool FIN>
+__device__ __forceinline__ void iter_block(const IterArgs &a, unsigned bx, unsigned by, const GlibcTablesBP &tab,
+                                           double *hb) {
+    const int ft = 1 << a.g.lft;
+    const int nsub = 256 >> a.g.lft;
+    const int ld = a.ld;
+    const int f = (int)(by << a.g.lft) + (threadIdx.x & (ft - 1));
+    const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> a.g.lft);
+    const bool was = a.active[f] != 0;
+    const bool act = was && (!a.unsat_s || a.unsat_s[f] != 0);
+    int64_t ci = (int64_t)bx * a.g.per * nsub + sub;
+    if (ci == 0 && was && !act) {  // decoder.pyx:431-433 for iteration t-2
+        a.success[f] = 1;
+        a.iters[f] = a.status_iter;
+        a.active[f] = 0;
+    }
+    if (!wave_any(act)) return;
+    const auto K = Arith<kStrict>::regs();
+    const uint32_t b8 = (uint32_t)f * 8u;
+    uint32_t bad = 0;
+    for (int j = 0; j < a.g.per; ++j, ci += nsub) {
+        if (ci >= a.n_checks) break;
+        const int cc = sld(a.checks + ci);
+        const int base = sld(a.chk_ptr + cc);
+        uint32_t par = *at_byte(row_ptr(a.synd, cc, ld), (uint32_t)f);
+        double m[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            const int v = sld(a.chk_var + base + i), e = sld(a.chk_edge + base + i);
+            const int vb = sld(a.var_ptr + v), ve = sld(a.var_ptr + v + 1);
+            double p = ld_row<NT>(row_ptr(a.lappr, v, ld), b8, ld);
+            double own = 0.0;
+            for (int k = vb; k < ve; ++k) {  // decoder.pyx:292-293, ascending edge id
+                const int ek = sld(a.var_edge + k);
+                const double c = a.c2v_in ? ld_row<false>(row_ptr(a.c2v_in, ek, ld), b8, ld) : 0.0;
+                p += c;
+                own = (ek == e) ? c : own;
+            }
+            if (act && sld(a.var_edge + vb) == e) st_row<false>(row_ptr(a.post, v, ld), b8, ld, p);
+            par ^= (p < 0.0) ? 1u : 0u;  // decoder.pyx:243-246
+            m[i] = p - own;              // :296-297
+        }
+        bad |= (par == 1u) ? 1u : 0u;
+        if (a.c2v_out) {
+            const double s = *at_byte(row_ptr(a.synd, cc, ld), (uint32_t)f) ? -1.0 : 1.0;
+            double out[D];
+            double *wb = hb + (threadIdx.x >> 6) * kPackWaveDoubles;
+            check_strict_packed<D, FIN ? kClampFinite : kClampFull>(m, out, wb, tab, K);
+#pragma unroll
+            for (int i = 0; i < D; ++i)
+                if (act) st_row<NT>(row_ptr(a.c2v_out, sld(a.chk_edge + base + i), ld), b8, ld, s * out[i]);
+        }
+    }
+    if (a.unsat_p && bad && act) a.unsat_p[f] = 1;  // benign race: every writer stores 1
+}
+
+template <int D, bool NT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) k_iter(IterArgs a) {
+    __shared__ GlibcTablesBP tab;
+    __shared__ double hb[4 * kPackWaveDoubles];
+    if (a.c2v_out) stage_glibc_tables(&tab, a.gglibc);
+    if (a.finite && sld(a.finite)) iter_block<D, NT, true>(a, blockIdx.x, blockIdx.y, tab, hb);
+    else iter_block<D, NT, false>(a, blockIdx.x, blockIdx.y, tab, hb);
 }
 
 // One launch = the check sweep of one frame half and the variable sweep of the
@@ -649,19 +799,35 @@ __global__ void __launch_bounds__(1024) k_compact(int f0, int f1, uint8_t *__res
 // ------------------------------------------------------------------ launch
 struct DecodeWs {
     double *c2v;
+    double *c2v2;    // the second message buffer of the fused small-code schedule (run_iter), or null
     uint8_t *active;
     uint8_t *unsat;  // (max_it + 2) rows of ld flags
     double *fb;      // F scratch of the runtime-degree classes (fb_rows rows of ld), or null
     int32_t *alist;  // active-frame lists of the frame ranges (ld entries)
     int32_t *acount; // their lengths: [0] range starting at frame 0, [1] the second half;
                      // [2] the finite flag of the input LAPPRs (first variable sweep)
+    unsigned *queue; // work-queue heads of the check launches: slot (2 row + half) x classes + class
 };
+
+// Codes the one-launch-per-iteration schedule (k_iter) can run: one check-degree class of a
+// packed degree, bounded variable degrees, and messages small enough to double-buffer.
+static bool iter_code(const qr_code *code, int ld) {
+    return code->classes.size() == 1 && code->classes[0].degree >= 2 && code->classes[0].degree <= kPackMaxDeg &&
+           code->max_dv <= 64 && (size_t)code->E * ld * sizeof(double) <= ((size_t)1 << 30);
+}
+
+// Work-queue heads of the check launches: one per (row = t - 1, frame half, degree class).
+static size_t queue_slots(const qr_code *code, int max_it) {
+    const int64_t rows = (int64_t)(max_it > 0 ? max_it : 0) + 2;
+    return (size_t)rows * 2 * std::max<size_t>(1, code->classes.size());
+}
 
 static size_t ws_bytes(const qr_code *code, int ld, int max_it) {
     const int64_t rows = (int64_t)(max_it > 0 ? max_it : 0) + 2;  // no int overflow at INT_MAX
-    return align_up((size_t)code->E * ld * sizeof(double), 256) + align_up((size_t)ld, 256) +
+    const size_t msg = align_up((size_t)code->E * ld * sizeof(double), 256);
+    return msg + (iter_code(code, ld) ? msg : 0) + align_up((size_t)ld, 256) +
            align_up((size_t)rows * ld, 256) + align_up((size_t)code->fb_rows * ld * sizeof(double), 256) +
-           align_up((size_t)ld * sizeof(int32_t), 256) + 256;
+           align_up((size_t)ld * sizeof(int32_t), 256) + 256 + align_up(queue_slots(code, max_it) * sizeof(unsigned), 256);
 }
 
 static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
@@ -670,6 +836,11 @@ static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
     const int64_t rows = (int64_t)(max_it > 0 ? max_it : 0) + 2;  // no int overflow at INT_MAX
     w.c2v = (double *)p;
     p += align_up((size_t)code->E * ld * sizeof(double), 256);
+    w.c2v2 = nullptr;
+    if (iter_code(code, ld)) {
+        w.c2v2 = (double *)p;
+        p += align_up((size_t)code->E * ld * sizeof(double), 256);
+    }
     w.active = (uint8_t *)p;
     p += align_up((size_t)ld, 256);
     w.unsat = (uint8_t *)p;
@@ -679,6 +850,8 @@ static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
     w.alist = (int32_t *)p;
     p += align_up((size_t)ld * sizeof(int32_t), 256);
     w.acount = (int32_t *)p;
+    p += 256;
+    w.queue = (unsigned *)p;
     return w;
 }
 
@@ -686,7 +859,7 @@ static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
 struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3}, math{kStrict}, eps_max{40},
         lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024}, var_pace{28},
-        check_tail{4};
+        check_tail{4}, fused_iter{1}, check_queue{1}, queue_wgs{4};
 };
 static Tuning g_tune;
 
@@ -753,6 +926,9 @@ struct Plan {
         a.finite = w.acount + 2;
         a.nmain = 0;
         a.per_t = a.g.per;
+        a.queue = nullptr;
+        a.ntiles = (unsigned)((f1 - f0) >> a.g.lft);
+        a.nbx_t = a.nbx;
         return a;
     }
     VarArgs var_args(int f0, int f1) const {
@@ -787,6 +963,18 @@ struct Plan {
         default: handled = false;                                                                            \
     }
 
+// Workgroups of a work-queue check sweep: queue_wgs (default 4: the strict check kernel's
+// residency at <= 128 VGPRs) per CU; more would only dequeue nothing.
+static int64_t resident_check_blocks(int device) {
+    static std::atomic<int> cus[64];
+    int cu = (device >= 0 && device < 64) ? cus[device].load() : 0;
+    if (cu <= 0) {
+        if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cu <= 0) cu = 256;
+        if (device >= 0 && device < 64) cus[device].store(cu);
+    }
+    return (int64_t)cu * std::max(1, g_tune.queue_wgs.load());
+}
+
 // Arithmetic of the check launches (knob math); parity-only sweeps need no tables.
 static int math_mode(int mode) {
     const int m = g_tune.math.load();
@@ -807,7 +995,18 @@ static int launch_check_class(const Plan &P, const DegreeClass &cls, const doubl
     // knob check_tail (default 4; 0 = off; MI355X: +1 %): frame tile 0 is swept last with per / check_tail
     // checks per thread (the templated degrees only; the runtime-degree kernel keeps the 2-D grid)
     const int tail = g_tune.check_tail.load();
-    if (tail > 1 && grid.y >= 2 && cls.degree <= kMaxTemplDeg && a.g.per >= tail) {
+    const bool templ = cls.degree >= 2 && cls.degree <= kMaxTemplDeg;
+    if (g_tune.check_queue.load() && MODE != kParityOnly && templ && P.w.queue) {
+        // work queue: one head per (row t - 1 = the unsat row of this sweep, frame half, class)
+        const int64_t row = (int64_t)(unsat - P.w.unsat) / P.ld;
+        const int64_t k = &cls - P.code->classes.data();
+        a.queue = P.w.queue + (2 * row + (f0 != 0 ? 1 : 0)) * (int64_t)P.code->classes.size() + k;
+        a.per_t = (tail > 1 && a.g.per >= tail) ? a.g.per / tail : a.g.per;
+        const int64_t per_block_t = (int64_t)a.per_t * (256 >> a.g.lft);
+        a.nbx_t = (unsigned)((cls.n + per_block_t - 1) / per_block_t);
+        const int64_t items = (int64_t)(a.ntiles - 1) * a.nbx + a.nbx_t;
+        grid = dim3((unsigned)std::min<int64_t>(items, resident_check_blocks(P.code->device)), 1);
+    } else if (tail > 1 && grid.y >= 2 && templ && a.g.per >= tail) {
         const int64_t per_block_t = (int64_t)(a.g.per / tail) * (256 >> a.g.lft);
         const int64_t nbx_t = (cls.n + per_block_t - 1) / per_block_t;
         a.nmain = a.nbx * (grid.y - 1);
@@ -1111,6 +1310,55 @@ static int run_split2(const Plan &P, int max_it) {
     return QR_OK;
 }
 
+// The one-launch-per-iteration schedule of small codes (k_iter): P(1) .. P(max_it + 1), the last
+// one the final parity sweep.
+static int run_iter(const Plan &P, int max_it) {
+    const DegreeClass &cls = P.code->classes[0];
+    const int ld = P.ld;
+    IterArgs a;
+    a.checks = cls.d_checks;
+    a.n_checks = cls.n;
+    a.chk_ptr = P.code->d_chk_ptr;
+    a.chk_edge = P.code->d_chk_edge;
+    a.chk_var = P.code->d_chk_var;
+    a.var_ptr = P.code->d_var_ptr;
+    a.var_edge = P.code->d_var_edge;
+    a.lappr = P.lappr;
+    a.post = P.post;
+    a.synd = P.synd;
+    a.active = P.w.active;
+    a.success = P.success;
+    a.iters = P.iters;
+    a.ld = ld;
+    a.g = make_geom(ld, g_tune.check_ft.load(), g_tune.check_per.load(), cls.n);
+    const int64_t per_block = (int64_t)a.g.per * (256 >> a.g.lft);
+    a.nbx = (unsigned)((cls.n + per_block - 1) / per_block);
+    a.gglibc = P.code->d_gtab;
+    a.finite = P.w.acount + 2;
+    const dim3 grid(a.nbx, (unsigned)(ld >> a.g.lft));
+    double *buf[2] = {P.w.c2v, P.w.c2v2};
+    for (int t = 1; t <= max_it + 1; ++t) {
+        a.c2v_in = t == 1 ? nullptr : buf[(t - 1) & 1];
+        a.c2v_out = t <= max_it ? buf[t & 1] : nullptr;
+        a.unsat_s = t >= 3 ? P.w.unsat + (size_t)(t - 2) * ld : nullptr;
+        a.unsat_p = t >= 2 ? P.w.unsat + (size_t)(t - 1) * ld : nullptr;
+        a.status_iter = t - 2;
+        ProfScope ps(profiling_on() ? "iter_d" + std::to_string(cls.degree) : std::string(), P.s);
+#define QR_CASE(DD)                                                                     \
+    case DD:                                                                            \
+        if (P.nt) k_iter<DD, true><<<grid, 256, 0, P.s>>>(a);                           \
+        else k_iter<DD, false><<<grid, 256, 0, P.s>>>(a);                               \
+        break;
+        switch (cls.degree) {
+            QR_CASE(2) QR_CASE(3) QR_CASE(4) QR_CASE(5) QR_CASE(6) QR_CASE(7) QR_CASE(8) QR_CASE(9) QR_CASE(10)
+            default: return set_error(QR_EVALUE, "decode: no fused-iteration kernel for degree %d", cls.degree);
+        }
+#undef QR_CASE
+        QR_LAUNCH_CHECK();
+    }
+    return QR_OK;
+}
+
 int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr, const uint8_t *synd, int max_it,
                         double *final_post, uint8_t *success, int32_t *iters, void *ws_ptr, size_t ws_size,
                         hipStream_t s) {
@@ -1125,6 +1373,7 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     const int64_t rows = (int64_t)(max_it > 0 ? max_it : 0) + 2;  // no int overflow at INT_MAX
     int rc;
     QR_HIP(hipMemsetAsync(P.w.unsat, 0, (size_t)rows * ld, s));
+    QR_HIP(hipMemsetAsync(P.w.queue, 0, queue_slots(code, max_it) * sizeof(unsigned), s));
     k_init_status<<<(ld + 255) / 256, 256, 0, s>>>(B, ld, P.w.active, success, iters, P.w.acount + 2);
     QR_LAUNCH_CHECK();
     // the strict arithmetic's finite flag: bound 2^e with e = 1000 - (max_it + 2) log2(dv_max + 1)
@@ -1152,6 +1401,12 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     const int64_t half_blocks = (max_n + (int64_t)gh.per * (256 >> gh.lft) - 1) / ((int64_t)gh.per * (256 >> gh.lft)) *
                                 ((ld / 2) >> gh.lft);
     const bool split = sp >= 2 && ld % 512 == 0 && max_deg <= 16 && half_blocks >= g_tune.split_min_blocks.load();
+    const bool iter = !split && max_it > 0 && g_tune.fused_iter.load() && P.w.c2v2 && math_mode(kNormal) == kStrict;
+    if (iter) {
+        if ((rc = run_iter(P, max_it))) return rc;
+        // P(max_it + 1) was the parity sweep of the last posteriors; every frame still running stops
+        return launch_status(P, 0, ld, max_it, 1, max_it, P.w.unsat + (size_t)max_it * ld);
+    }
     // active-frame lists of the ranges the schedule sweeps (after the iteration-0 status)
     P.compact = g_tune.compact.load() != 0;
     if (split) {
@@ -1358,6 +1613,8 @@ static std::atomic<int> *tune_knob(const char *name) {
         {"demap_hyp", &g_demap_hyp},        {"min_blocks", &g_tune.min_blocks},
         {"split_min_blocks", &g_tune.split_min_blocks},
         {"var_pace", &g_tune.var_pace},     {"check_tail", &g_tune.check_tail},
+        {"fused_iter", &g_tune.fused_iter}, {"check_queue", &g_tune.check_queue},
+        {"queue_wgs", &g_tune.queue_wgs},
     };
     const std::string n = name ? name : "";
     for (const auto &k : knobs)

@@ -216,6 +216,80 @@ k_demap_hyp(const DemapTables *__restrict__ tab,
     }
 }
 
+// ---------------------------------------------------------------------------
+// Wave-private demapper (knob demap_hyp = 3): the same per-(frame, hypothesis) work as
+// k_demap_hyp, but ONE wave walks all M hypotheses of its own 64-frame tile (lane = frame) and
+// keeps the Gray-labelled sums N[k] / D[k] of its lanes in a wave-private LDS slice, updated
+// in i order (noisemapper.pyx:521-530: per bit the reference's sequence of additions).  No
+// workgroup barrier: a wave's search lengths never hold up another wave.  The exact F_Y of the
+// closed-form root search is evaluated by the whole wave as in g_inv_search_wave.
+template <int BPS>
+__global__ void __launch_bounds__(256) k_demap_wave(const DemapTables *__restrict__ tab,
+                                                    const MathTables *__restrict__ gmt, int B, int ld, int64_t S,
+                                                    const double *__restrict__ n, const int64_t *__restrict__ j,
+                                                    double alpha, double *__restrict__ lappr) {
+    constexpr int M = 1 << BPS;
+    __shared__ GlibcExpLog gt;
+    __shared__ double ey[4][64], et[4][64];
+    __shared__ double acc[4][2 * BPS][64];   // per wave: N[k] rows then D[k] rows, lane = frame
+    stage_glibc_exp_log(&gt, &kGlibcConst);
+    const DemapTables &t = *tab;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double *accw = &acc[w][0][0];
+    const int64_t tiles = ld / 64;
+    const int64_t items = S * tiles;
+    for (int64_t it = (int64_t)blockIdx.x * 4 + w; it < items; it += (int64_t)gridDim.x * 4) {   // wave-uniform
+        const int64_t s = it / tiles;
+        const int f = (int)(it - s * tiles) * 64 + lane;
+        const bool valid = f < B;
+        const double nv = valid ? n[s * ld + f] : 0.5;   // padding lanes: a harmless target
+        const int64_t jv = valid ? j[s * ld + f] : 0;
+        const bool jok = jv >= 0 && jv < M;
+        const int jj = jok ? (int)jv : 0;
+        const double aj = t.a[jj];
+#pragma unroll
+        for (int k = 0; k < 2 * BPS; ++k) accw[k * 64 + lane] = 0.0;
+#pragma unroll 1
+        for (int i = 0; i < M; ++i) {
+            const double y = g_inv_search_wave<M>(t, *gmt, nv, i, ey[w], et[w], lane);
+            // noisemapper.pyx:503-515 in the reference's summation order (k < j, p[j], k > j)
+            double sum = 0;
+#pragma unroll QR_DEMAP_HYP_UNROLL
+            for (int k = 0; k < M; ++k) {
+                const double e = (2 * y - t.a[k] - aj) * (t.a[k] - aj);
+                const double arg = k < jj ? e : k == jj ? 1.0 : div_two_s2(t, e);
+                const double ex = g_exp_wave(arg, gt);
+                sum += k == jj ? t.p[jj] : ex * t.p[k];
+            }
+            const double q = t.dF[i] / sum;
+            int mi = i;
+#pragma unroll
+            for (int k = 0; k < BPS; ++k) {   // noisemapper.pyx:521-530: Gray bit k of i
+                double *a = accw + (((mi * (mi + 1)) & 3) ? BPS + k : k) * 64 + lane;
+                *a += q;
+                mi >>= 1;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < BPS; ++k) {
+            const double out = (g_log_full(accw[k * 64 + lane], gt) - g_log_full(accw[(BPS + k) * 64 + lane], gt)) *
+                               alpha;   // :534-538, x alpha
+            if (valid) lappr[(s * BPS + k) * ld + f] = jok ? out : __builtin_nan("");
+        }
+    }
+}
+
+static bool launch_demap_wave(int bps, unsigned grid, hipStream_t st, const qr_demap *dm, int B, int ld, int64_t S,
+                              const double *n, const int64_t *j, double alpha, double *lappr) {
+    switch (bps) {
+#define QR_DEMAP_WAVE(b) \
+        case b: k_demap_wave<b><<<grid, 256, 0, st>>>(dm->d_tables, dm->d_mtab, B, ld, S, n, j, alpha, lappr); return true;
+        QR_DEMAP_WAVE(1) QR_DEMAP_WAVE(2) QR_DEMAP_WAVE(3) QR_DEMAP_WAVE(4) QR_DEMAP_WAVE(5) QR_DEMAP_WAVE(6)
+#undef QR_DEMAP_WAVE
+        default: return false;
+    }
+}
+
 // workgroups of the grid-stride demap: enough to fill every CU several times over
 static unsigned demap_hyp_grid(int device, int64_t items) {
     static std::atomic<int> cus[64];
@@ -463,7 +537,9 @@ int demap_batch_device(const qr_demap *dm, int B, int ld, int64_t S, const doubl
     if (fast && (hyp >= 2 || (hyp == 1 && dm->h.bps >= kDemapHypAutoBps)) && ld % kWave == 0 &&
         dm->h.bps <= kDemapHypMaxBps) {
         const int64_t items = S * (ld / kWave);
-        launch_demap_hyp(dm->h.bps, demap_hyp_grid(dm->device, items), s, dm, B, ld, S, n, j, alpha, lappr);
+        if (hyp == 3) launch_demap_wave(dm->h.bps, demap_hyp_grid(dm->device, (items + 3) / 4), s, dm, B, ld, S, n, j,
+                                        alpha, lappr);
+        else launch_demap_hyp(dm->h.bps, demap_hyp_grid(dm->device, items), s, dm, B, ld, S, n, j, alpha, lappr);
     } else {
         const int64_t items = S * ld;
         launch_demap_bps(dm->h.bps, fast, (unsigned)((items + 255) / 256), s, dm, B, ld, S, n, j, alpha, lappr);

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
-"""A/B of the demapper kernels on the GPU: hypothesis-parallel (demap_hyp=2; the default 1 picks it from 16-PAM up)
-vs one lane per symbol (demap_hyp=0), both with the fast root search, at the bench's
-batch (B = 4096 frames, N = 64800): ms per launch (hipEvents, median of reps) and
-bit-identity of the LAPPRs.   python scripts/demap_ab.py [--batch 4096] [--reps 3]"""
+"""A/B of the demapper kernels on the GPU at the bench's batch (B = 4096 frames, N = 64800):
+demap_hyp = 3 (wave-private: one wave walks all hypotheses of its tile), 2 (hypothesis-parallel,
+LDS combine), 0 (one lane per symbol), all with the fast root search: ms per launch (hipEvents,
+median of reps) and bit-identity of the LAPPRs.
+    python scripts/demap_ab.py [--batch 4096] [--reps 3] [--variants 3,2,0]"""
 import argparse
 import json
 import os
@@ -15,7 +16,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--cases", default="2:3.0,2:9.5,4:13.0,4:14.5,4:25.0")
+    ap.add_argument("--cases", default="2:3.0,4:13.0,4:14.5,4:25.0")
+    ap.add_argument("--variants", default="3,2,0")
     args = ap.parse_args()
     import torch
     import qamr
@@ -24,13 +26,15 @@ def main():
 
     vid, cid = codes.dvbs2_like_half()
     dec = qamr.Decoder(vid, cid)
+    variants = [int(v) for v in args.variants.split(",")]
+    saved = _lib.tune_get("demap_hyp")
     rows = []
     for case in args.cases.split(","):
         bps, snr = int(case.split(":")[0]), float(case.split(":")[1])
         pipe = SofteningPipeline(dec, bps, snr, batch=args.batch, max_iterations=1)
         b = pipe.generate(torch.Generator(device="cuda").manual_seed(0))
         out, ms = {}, {}
-        for hyp in (2, 0):
+        for hyp in variants:
             _lib.tune_set("demap_hyp", hyp)
             o = pipe.demap(b)  # warm
             t = []
@@ -41,12 +45,12 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 t.append(e0.elapsed_time(e1))
-            ms[min(hyp, 1)] = sorted(t)[len(t) // 2]
-            out[min(hyp, 1)] = o
-        _lib.tune_set("demap_hyp", 1)
-        same = torch.equal(out[0].view(torch.int64), out[1].view(torch.int64))
-        r = {"bps": bps, "snr": snr, "B": b.B, "hyp_ms": round(ms[1], 3), "per_symbol_ms": round(ms[0], 3),
-             "speedup": round(ms[0] / ms[1], 3), "bit_identical": same}
+            ms[hyp] = round(sorted(t)[len(t) // 2], 3)
+            out[hyp] = o
+        _lib.tune_set("demap_hyp", saved)
+        ref = out[variants[-1]].view(torch.int64)
+        same = all(torch.equal(out[v].view(torch.int64), ref) for v in variants)
+        r = {"bps": bps, "snr": snr, "B": b.B, "ms_by_demap_hyp": ms, "bit_identical": same}
         rows.append(r)
         print(json.dumps(r), flush=True)
         del pipe, b, out

@@ -212,17 +212,22 @@ def test_hypothesis_parallel_demap_equals_per_symbol(gpu, bps, snr):
     dev = torch.device("cuda", 0)
     nt = torch.from_numpy(n).to(dev).contiguous()
     xt = torch.from_numpy(x).to(dev).contiguous()
+    saved = _lib.tune_get("demap_hyp")
     try:
         _lib.tune_set("demap_hyp", 2)   # hypothesis-parallel for every order
         hyp = nm.demap_device(nt, xt, B, alpha=0.5).clone()
+        _lib.tune_set("demap_hyp", 3)   # wave-private: one wave walks all hypotheses of its tile
+        wav = nm.demap_device(nt, xt, B, alpha=0.5).clone()
         _lib.tune_set("demap_hyp", 0)
         per = nm.demap_device(nt, xt, B, alpha=0.5).clone()
     finally:
-        _lib.tune_set("demap_hyp", 1)
+        _lib.tune_set("demap_hyp", saved)
     torch.cuda.synchronize()
-    a, b = hyp[:, :B].cpu().numpy(), per[:, :B].cpu().numpy()
-    same = (a.view(np.int64) == b.view(np.int64)) | (np.isnan(a) & np.isnan(b))
-    assert same.all(), f"{(~same).sum()} LAPPRs differ"
+    b = per[:, :B].cpu().numpy()
+    for out in (wav, hyp):
+        a = out[:, :B].cpu().numpy()
+        same = (a.view(np.int64) == b.view(np.int64)) | (np.isnan(a) & np.isnan(b))
+        assert same.all(), f"{(~same).sum()} LAPPRs differ"
     assert np.isnan(a[bps:2 * bps, :3]).all()
     if bps <= 4:
         onm = O.OracleNoiseMapper(bps, 2.0, nv, cfg)
