@@ -614,6 +614,81 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
     else iter_block<D, NT, false>(a, blockIdx.x, blockIdx.y, tab, hb);
 }
 
+// The same iterations in ONE persistent launch (knob fused_iter = 2): the workgroups are split
+// into `groups` groups, group g sweeping the frame tiles g, g + groups, ...; a frame's sweeps
+// only depend on the same frame's data, so the phases P(t) -> P(t+1) of a group are separated
+// by a barrier among that group's workgroups alone (release fence -> arrival counter -> poll
+// -> acquire fence, MI355X_MICROARCH.md 'Valid forms').  The grid is sized to the resident
+// workgroups; every wait is bounded: past kBarrierSpin polls the workgroup sets *abort and
+// leaves (no hung wave), and the decode then reports iterations -1 for every frame.
+struct PersistArgs {
+    double *buf0, *buf1;   // c2v ping-pong buffers
+    uint8_t *unsat;        // row 0 of the per-iteration parity flags
+    int max_it;
+    unsigned groups;
+    unsigned *bar;         // [groups] monotonic arrival counters, zero at launch
+    unsigned *abort;
+};
+constexpr unsigned kBarrierSpin = 1u << 22;
+
+__device__ __forceinline__ bool group_barrier(unsigned *ctr, unsigned target, unsigned *abort) {
+    __shared__ int s_ok;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have completed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int ok = 1;
+        for (unsigned spin = 0;; ++spin) {
+            if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+            if ((spin & 255u) == 255u &&
+                (spin >= kBarrierSpin || __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_ok = ok;
+    }
+    __syncthreads();
+    return s_ok != 0;
+}
+
+template <int D, bool NT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) k_iter_persist(IterArgs a,
+                                                                                                 PersistArgs p) {
+    __shared__ GlibcTablesBP tab;
+    __shared__ double hb[4 * kPackWaveDoubles];
+    stage_glibc_tables(&tab, a.gglibc);
+    const unsigned G = p.groups, g = blockIdx.x % G, r = blockIdx.x / G, wpg = gridDim.x / G;
+    if (r >= wpg) return;  // (gridDim.x is a multiple of G: never)
+    const unsigned ntiles = (unsigned)(a.ld >> a.g.lft);
+    const bool fin = a.finite && sld(a.finite);
+    for (int t = 1; t <= p.max_it + 1; ++t) {
+        IterArgs b = a;
+        b.c2v_in = t == 1 ? nullptr : (((t - 1) & 1) ? p.buf1 : p.buf0);
+        b.c2v_out = t <= p.max_it ? ((t & 1) ? p.buf1 : p.buf0) : nullptr;
+        b.unsat_s = t >= 3 ? p.unsat + (size_t)(t - 2) * a.ld : nullptr;
+        b.unsat_p = t >= 2 ? p.unsat + (size_t)(t - 1) * a.ld : nullptr;
+        b.status_iter = t - 2;
+        for (unsigned by = g; by < ntiles; by += G)
+            for (unsigned bx = r; bx < a.nbx; bx += wpg) {
+                if (fin) iter_block<D, NT, true>(b, bx, by, tab, hb);
+                else iter_block<D, NT, false>(b, bx, by, tab, hb);
+            }
+        if (t <= p.max_it && !group_barrier(p.bar + g, wpg * (unsigned)t, p.abort)) return;
+    }
+}
+
+__global__ void k_persist_abort_check(const unsigned *abort, int B, int32_t *iters) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f < B && *abort) iters[f] = -1;
+}
+
 // One launch = the check sweep of one frame half and the variable sweep of the
 // other (they never touch the same frame columns).  The check sweep is VALU heavy
 // and the variable sweep HBM bound: interleaving their workgroups (evenly spread
@@ -819,7 +894,7 @@ static bool iter_code(const qr_code *code, int ld) {
 // Work-queue heads of the check launches: one per (row = t - 1, frame half, degree class).
 static size_t queue_slots(const qr_code *code, int max_it) {
     const int64_t rows = (int64_t)(max_it > 0 ? max_it : 0) + 2;
-    return (size_t)rows * 2 * std::max<size_t>(1, code->classes.size());
+    return std::max<size_t>(16, (size_t)rows * 2 * std::max<size_t>(1, code->classes.size()));
 }
 
 static size_t ws_bytes(const qr_code *code, int ld, int max_it) {
@@ -1312,7 +1387,7 @@ static int run_split2(const Plan &P, int max_it) {
 
 // The one-launch-per-iteration schedule of small codes (k_iter): P(1) .. P(max_it + 1), the last
 // one the final parity sweep.
-static int run_iter(const Plan &P, int max_it) {
+static int run_iter(const Plan &P, int max_it, bool persist) {
     const DegreeClass &cls = P.code->classes[0];
     const int ld = P.ld;
     IterArgs a;
@@ -1337,6 +1412,29 @@ static int run_iter(const Plan &P, int max_it) {
     a.finite = P.w.acount + 2;
     const dim3 grid(a.nbx, (unsigned)(ld >> a.g.lft));
     double *buf[2] = {P.w.c2v, P.w.c2v2};
+    if (persist) {
+        // groups of frame tiles (at most 8: blocks b and b + 8 share an XCD, so a group's barrier
+        // and its tiles' messages stay on one XCD when the dispatcher deals blocks round-robin)
+        const unsigned tiles = (unsigned)(ld >> a.g.lft);
+        const unsigned G = std::min(8u, tiles);
+        const unsigned wpg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(resident_check_blocks(P.code->device) / G,
+                                                                               (int64_t)a.nbx * ((tiles + G - 1) / G)));
+        PersistArgs pa{buf[0], buf[1], P.w.unsat, max_it, G, P.w.queue, P.w.queue + 8};   // 8 >= G
+        QR_HIP(hipMemsetAsync(P.w.queue, 0, 9 * sizeof(unsigned), P.s));
+        ProfScope ps(profiling_on() ? "persist_d" + std::to_string(cls.degree) : std::string(), P.s);
+#define QR_CASE(DD)                                                                     \
+    case DD:                                                                            \
+        if (P.nt) k_iter_persist<DD, true><<<G * wpg, 256, 0, P.s>>>(a, pa);            \
+        else k_iter_persist<DD, false><<<G * wpg, 256, 0, P.s>>>(a, pa);                \
+        break;
+        switch (cls.degree) {
+            QR_CASE(2) QR_CASE(3) QR_CASE(4) QR_CASE(5) QR_CASE(6) QR_CASE(7) QR_CASE(8) QR_CASE(9) QR_CASE(10)
+            default: return set_error(QR_EVALUE, "decode: no fused-iteration kernel for degree %d", cls.degree);
+        }
+#undef QR_CASE
+        QR_LAUNCH_CHECK();
+        return QR_OK;
+    }
     for (int t = 1; t <= max_it + 1; ++t) {
         a.c2v_in = t == 1 ? nullptr : buf[(t - 1) & 1];
         a.c2v_out = t <= max_it ? buf[t & 1] : nullptr;
@@ -1403,9 +1501,15 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     const bool split = sp >= 2 && ld % 512 == 0 && max_deg <= 16 && half_blocks >= g_tune.split_min_blocks.load();
     const bool iter = !split && max_it > 0 && g_tune.fused_iter.load() && P.w.c2v2 && math_mode(kNormal) == kStrict;
     if (iter) {
-        if ((rc = run_iter(P, max_it))) return rc;
+        const bool persist = g_tune.fused_iter.load() == 2;
+        if ((rc = run_iter(P, max_it, persist))) return rc;
         // P(max_it + 1) was the parity sweep of the last posteriors; every frame still running stops
-        return launch_status(P, 0, ld, max_it, 1, max_it, P.w.unsat + (size_t)max_it * ld);
+        if ((rc = launch_status(P, 0, ld, max_it, 1, max_it, P.w.unsat + (size_t)max_it * ld))) return rc;
+        if (persist) {  // a barrier wait that timed out (never expected) marks every frame
+            k_persist_abort_check<<<(B + 255) / 256, 256, 0, s>>>(P.w.queue + 8, B, iters);
+            QR_LAUNCH_CHECK();
+        }
+        return QR_OK;
     }
     // active-frame lists of the ranges the schedule sweeps (after the iteration-0 status)
     P.compact = g_tune.compact.load() != 0;
