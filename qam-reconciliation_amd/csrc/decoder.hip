@@ -549,7 +549,9 @@ struct IterArgs {
     const int32_t *finite;
 };
 
-template <int D, bool NT, bool FIN>
+// Every access is cached (no non-temporal hint): a small code's messages, posteriors and LAPPRs
+// are re-read every iteration from L2 / MALL.
+template <int D, bool FIN>
 __device__ __forceinline__ void iter_block(const IterArgs &a, unsigned bx, unsigned by, const GlibcTablesBP &tab,
                                            double *hb) {
     const int ft = 1 << a.g.lft;
@@ -579,7 +581,7 @@ __device__ __forceinline__ void iter_block(const IterArgs &a, unsigned bx, unsig
         for (int i = 0; i < D; ++i) {
             const int v = sld(a.chk_var + base + i), e = sld(a.chk_edge + base + i);
             const int vb = sld(a.var_ptr + v), ve = sld(a.var_ptr + v + 1);
-            double p = ld_row<NT>(row_ptr(a.lappr, v, ld), b8, ld);
+            double p = ld_row<false>(row_ptr(a.lappr, v, ld), b8, ld);
             double own = 0.0;
             for (int k = vb; k < ve; ++k) {  // decoder.pyx:292-293, ascending edge id
                 const int ek = sld(a.var_edge + k);
@@ -599,19 +601,19 @@ __device__ __forceinline__ void iter_block(const IterArgs &a, unsigned bx, unsig
             check_strict_packed<D, FIN ? kClampFinite : kClampFull>(m, out, wb, tab, K);
 #pragma unroll
             for (int i = 0; i < D; ++i)
-                if (act) st_row<NT>(row_ptr(a.c2v_out, sld(a.chk_edge + base + i), ld), b8, ld, s * out[i]);
+                if (act) st_row<false>(row_ptr(a.c2v_out, sld(a.chk_edge + base + i), ld), b8, ld, s * out[i]);
         }
     }
     if (a.unsat_p && bad && act) a.unsat_p[f] = 1;  // benign race: every writer stores 1
 }
 
-template <int D, bool NT>
+template <int D>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) k_iter(IterArgs a) {
     __shared__ GlibcTablesBP tab;
     __shared__ double hb[4 * kPackWaveDoubles];
     if (a.c2v_out) stage_glibc_tables(&tab, a.gglibc);
-    if (a.finite && sld(a.finite)) iter_block<D, NT, true>(a, blockIdx.x, blockIdx.y, tab, hb);
-    else iter_block<D, NT, false>(a, blockIdx.x, blockIdx.y, tab, hb);
+    if (a.finite && sld(a.finite)) iter_block<D, true>(a, blockIdx.x, blockIdx.y, tab, hb);
+    else iter_block<D, false>(a, blockIdx.x, blockIdx.y, tab, hb);
 }
 
 // The same iterations in ONE persistent launch (knob fused_iter = 2): the workgroups are split
@@ -658,7 +660,7 @@ __device__ __forceinline__ bool group_barrier(unsigned *ctr, unsigned target, un
     return s_ok != 0;
 }
 
-template <int D, bool NT>
+template <int D>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) k_iter_persist(IterArgs a,
                                                                                                  PersistArgs p) {
     __shared__ GlibcTablesBP tab;
@@ -677,8 +679,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
         b.status_iter = t - 2;
         for (unsigned by = g; by < ntiles; by += G)
             for (unsigned bx = r; bx < a.nbx; bx += wpg) {
-                if (fin) iter_block<D, NT, true>(b, bx, by, tab, hb);
-                else iter_block<D, NT, false>(b, bx, by, tab, hb);
+                if (fin) iter_block<D, true>(b, bx, by, tab, hb);
+                else iter_block<D, false>(b, bx, by, tab, hb);
             }
         if (t <= p.max_it && !group_barrier(p.bar + g, wpg * (unsigned)t, p.abort)) return;
     }
@@ -1424,8 +1426,7 @@ static int run_iter(const Plan &P, int max_it, bool persist) {
         ProfScope ps(profiling_on() ? "persist_d" + std::to_string(cls.degree) : std::string(), P.s);
 #define QR_CASE(DD)                                                                     \
     case DD:                                                                            \
-        if (P.nt) k_iter_persist<DD, true><<<G * wpg, 256, 0, P.s>>>(a, pa);            \
-        else k_iter_persist<DD, false><<<G * wpg, 256, 0, P.s>>>(a, pa);                \
+        k_iter_persist<DD><<<G * wpg, 256, 0, P.s>>>(a, pa);                             \
         break;
         switch (cls.degree) {
             QR_CASE(2) QR_CASE(3) QR_CASE(4) QR_CASE(5) QR_CASE(6) QR_CASE(7) QR_CASE(8) QR_CASE(9) QR_CASE(10)
@@ -1444,8 +1445,7 @@ static int run_iter(const Plan &P, int max_it, bool persist) {
         ProfScope ps(profiling_on() ? "iter_d" + std::to_string(cls.degree) : std::string(), P.s);
 #define QR_CASE(DD)                                                                     \
     case DD:                                                                            \
-        if (P.nt) k_iter<DD, true><<<grid, 256, 0, P.s>>>(a);                           \
-        else k_iter<DD, false><<<grid, 256, 0, P.s>>>(a);                               \
+        k_iter<DD><<<grid, 256, 0, P.s>>>(a);                                           \
         break;
         switch (cls.degree) {
             QR_CASE(2) QR_CASE(3) QR_CASE(4) QR_CASE(5) QR_CASE(6) QR_CASE(7) QR_CASE(8) QR_CASE(9) QR_CASE(10)

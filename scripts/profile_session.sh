@@ -20,6 +20,7 @@ step() {  # step <name> <secs> <cmd...>
 if [[ ${SKIP_TRACE:-0} != 1 ]]; then
 step trace 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH ${TRACE_ARGS:-}
 fi
+[[ ${SKIP_PMC:-0} == 1 ]] && exit 0
 if [ -n "${PMC_GROUPS:-}" ]; then IFS=';' read -r -a GRPS <<< "$PMC_GROUPS"; else
 GRPS=("FETCH_SIZE" "WRITE_SIZE"
       "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
