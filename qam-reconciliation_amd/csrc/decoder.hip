@@ -448,29 +448,36 @@ __device__ __forceinline__ void check_queue(const CheckArgs &a, const typename A
         const unsigned k = s_item;
         __syncthreads();  // s_item is rewritten by the next dequeue
         if (k >= nitems) return;  // block-uniform
-        if (k < nfull) check_block<D, MODE, NT, AR, FIN>(a, k % a.nbx, k / a.nbx, a.g.per, tab, hb);
-        else check_block<D, MODE, NT, AR, FIN>(a, k - nfull, L - 1, a.per_t, tab, hb);
+        const bool tail = k >= nfull;  // one call site: one copy of the check body
+        check_block<D, MODE, NT, AR, FIN>(a, tail ? k - nfull : k % a.nbx, tail ? L - 1 : k / a.nbx,
+                                          tail ? a.per_t : a.g.per, tab, hb);
     }
+}
+
+// The work-queue sweep as a kernel of its own: its loop must not raise the register allocation
+// of the plain k_check (one kernel holding both bodies took 137 VGPRs: 3 waves per SIMD); the
+// strict queue kernel is held at 4 waves per SIMD (128 VGPRs; left alone it takes 132).
+template <int D, int MODE, bool NT, int AR>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AR == kStrict ? 4 : 1, 8))) k_check_q(CheckArgs a) {
+    __shared__ typename Arith<AR>::Tab tab;
+    __shared__ double hb[PackLds<AR>::doubles];
+#if QR_EXPERIMENT_CLOCK
+    ClkScope clk(D == 7 && MODE == kNormal && AR == kStrict);
+#endif
+    stage_tables<AR>(&tab, a);
+    if constexpr (kPacked<AR, D>) {
+        if (a.finite && sld(a.finite)) {  // kernel-uniform: one of the two bodies runs
+            check_queue<D, MODE, NT, AR, true>(a, tab, hb);
+            return;
+        }
+    }
+    check_queue<D, MODE, NT, AR, false>(a, tab, hb);
 }
 
 template <int D, int MODE, bool NT, int AR>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) k_check(CheckArgs a) {
     __shared__ typename Arith<AR>::Tab tab;
     __shared__ double hb[PackLds<AR>::doubles];
-    if (MODE != kParityOnly && a.queue) {
-#if QR_EXPERIMENT_CLOCK
-        ClkScope clk(D == 7 && MODE == kNormal && AR == kStrict);
-#endif
-        stage_tables<AR>(&tab, a);
-        if constexpr (kPacked<AR, D>) {
-            if (a.finite && sld(a.finite)) {  // kernel-uniform: one of the two bodies runs
-                check_queue<D, MODE, NT, AR, true>(a, tab, hb);
-                return;
-            }
-        }
-        check_queue<D, MODE, NT, AR, false>(a, tab, hb);
-        return;
-    }
     unsigned bx = blockIdx.x, by = blockIdx.y;
     int per = a.g.per;
     if (a.nmain) {  // short-tail 1-D grid (block-uniform)
@@ -1094,11 +1101,19 @@ static int launch_check_class(const Plan &P, const DegreeClass &cls, const doubl
                                       std::to_string(cls.degree)
                                 : std::string(),
                  P.s);
-#define QR_CASE(DD)                                                                    \
-    case DD:                                                                           \
-        if (ar == kStrict) k_check<DD, MODE, NT, kStrict><<<grid, 256, P.lds_pad, P.s>>>(a);   \
-        else if (ar == kEps) k_check<DD, MODE, NT, kEps><<<grid, 256, P.lds_pad, P.s>>>(a);    \
-        else k_check<DD, MODE, NT, kFast><<<grid, 256, P.lds_pad, P.s>>>(a);                   \
+#define QR_CASE(DD)                                                                                   \
+    case DD:                                                                                          \
+        if constexpr (MODE != kParityOnly) {                                                          \
+            if (a.queue) {                                                                            \
+                if (ar == kStrict) k_check_q<DD, MODE, NT, kStrict><<<grid, 256, P.lds_pad, P.s>>>(a); \
+                else if (ar == kEps) k_check_q<DD, MODE, NT, kEps><<<grid, 256, P.lds_pad, P.s>>>(a);  \
+                else k_check_q<DD, MODE, NT, kFast><<<grid, 256, P.lds_pad, P.s>>>(a);                 \
+                break;                                                                                \
+            }                                                                                         \
+        }                                                                                             \
+        if (ar == kStrict) k_check<DD, MODE, NT, kStrict><<<grid, 256, P.lds_pad, P.s>>>(a);          \
+        else if (ar == kEps) k_check<DD, MODE, NT, kEps><<<grid, 256, P.lds_pad, P.s>>>(a);           \
+        else k_check<DD, MODE, NT, kFast><<<grid, 256, P.lds_pad, P.s>>>(a);                          \
         break;
     bool handled = true;
     QR_DEG_SWITCH(cls.degree, QR_CASE, handled)
@@ -1387,6 +1402,36 @@ static int run_split2(const Plan &P, int max_it) {
     return QR_OK;
 }
 
+// One persistent launch (fused_iter = 2).  Every workgroup of the grid must be resident at once
+// (the group barriers wait for all of them): the grid is one workgroup per CU fewer than the
+// occupancy API grants this kernel (the API can grant one more than the hardware admits,
+// MI355X_MICROARCH.md 'Residency'), and the waits are bounded anyway.
+template <int D>
+static int launch_persist(const Plan &P, const IterArgs &a, int max_it, double *const *buf) {
+    static std::atomic<int> occ{0};
+    int per_cu = occ.load();
+    if (per_cu <= 0) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_iter_persist<D>, 256, 0) != hipSuccess || n <= 0) n = 2;
+        per_cu = std::max(1, n - 1);
+        occ.store(per_cu);
+    }
+    const int ld = P.ld;
+    // groups of frame tiles (at most 8: blocks b and b + 8 share an XCD, so a group's barrier and
+    // its tiles' messages stay on one XCD when the dispatcher deals blocks round-robin)
+    const unsigned tiles = (unsigned)(ld >> a.g.lft);
+    const unsigned G = std::min(8u, tiles);
+    const int64_t resident = resident_check_blocks(P.code->device) / std::max(1, g_tune.queue_wgs.load()) * per_cu;
+    const unsigned wpg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(resident / G,
+                                                                           (int64_t)a.nbx * ((tiles + G - 1) / G)));
+    PersistArgs pa{buf[0], buf[1], P.w.unsat, max_it, G, P.w.queue, P.w.queue + 8};   // 8 >= G
+    QR_HIP(hipMemsetAsync(P.w.queue, 0, 9 * sizeof(unsigned), P.s));
+    ProfScope ps(profiling_on() ? "persist_d" + std::to_string(D) : std::string(), P.s);
+    k_iter_persist<D><<<G * wpg, 256, 0, P.s>>>(a, pa);
+    QR_LAUNCH_CHECK();
+    return QR_OK;
+}
+
 // The one-launch-per-iteration schedule of small codes (k_iter): P(1) .. P(max_it + 1), the last
 // one the final parity sweep.
 static int run_iter(const Plan &P, int max_it, bool persist) {
@@ -1415,26 +1460,13 @@ static int run_iter(const Plan &P, int max_it, bool persist) {
     const dim3 grid(a.nbx, (unsigned)(ld >> a.g.lft));
     double *buf[2] = {P.w.c2v, P.w.c2v2};
     if (persist) {
-        // groups of frame tiles (at most 8: blocks b and b + 8 share an XCD, so a group's barrier
-        // and its tiles' messages stay on one XCD when the dispatcher deals blocks round-robin)
-        const unsigned tiles = (unsigned)(ld >> a.g.lft);
-        const unsigned G = std::min(8u, tiles);
-        const unsigned wpg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(resident_check_blocks(P.code->device) / G,
-                                                                               (int64_t)a.nbx * ((tiles + G - 1) / G)));
-        PersistArgs pa{buf[0], buf[1], P.w.unsat, max_it, G, P.w.queue, P.w.queue + 8};   // 8 >= G
-        QR_HIP(hipMemsetAsync(P.w.queue, 0, 9 * sizeof(unsigned), P.s));
-        ProfScope ps(profiling_on() ? "persist_d" + std::to_string(cls.degree) : std::string(), P.s);
-#define QR_CASE(DD)                                                                     \
-    case DD:                                                                            \
-        k_iter_persist<DD><<<G * wpg, 256, 0, P.s>>>(a, pa);                             \
-        break;
         switch (cls.degree) {
+#define QR_CASE(DD) \
+    case DD: return launch_persist<DD>(P, a, max_it, buf);
             QR_CASE(2) QR_CASE(3) QR_CASE(4) QR_CASE(5) QR_CASE(6) QR_CASE(7) QR_CASE(8) QR_CASE(9) QR_CASE(10)
+#undef QR_CASE
             default: return set_error(QR_EVALUE, "decode: no fused-iteration kernel for degree %d", cls.degree);
         }
-#undef QR_CASE
-        QR_LAUNCH_CHECK();
-        return QR_OK;
     }
     for (int t = 1; t <= max_it + 1; ++t) {
         a.c2v_in = t == 1 ? nullptr : buf[(t - 1) & 1];

@@ -21,19 +21,18 @@ namespace qr {
 
 // 1 = Newton-located root + replayed bisection (bit-identical, ~5x fewer erf), 0 = brute force.
 std::atomic<int> g_demap_fast{1};
-// Demap kernel on 64-frame tiles: 0 = one lane per symbol (k_demap), 2 = hypothesis-parallel
-// (k_demap_hyp) for every order, 1 (default) = hypothesis-parallel from 16-PAM up (measured on
-// MI355X, B = 4096: 16-PAM 46.8 vs 47.1 ms with no scratch traffic; 4-PAM 20.0 vs 13.9 ms).
+// Demap kernel on 64-frame tiles (knob demap_hyp): 1 (default) = wave-private (k_demap_wave: one
+// wave walks all M hypotheses of its 64-frame tile), 0 = one lane per symbol (k_demap).  Measured
+// on MI355X, B = 4096: 16-PAM 13 dB 44.2 vs 47.1 ms, 25 dB 52.2 vs 52.8 ms, 4-PAM 13.7 vs 13.8 ms;
+// the round-3 hypothesis-parallel kernel (waves split the hypotheses, two workgroup barriers per
+// symbol item) took 46.8 / 54.7 / 20.0 ms and was removed.
 std::atomic<int> g_demap_hyp{1};
-constexpr int kDemapHypAutoBps = 4;
 
-#ifndef QR_DEMAP_WAVES
-// Single-loop LLR sum: 5 waves/SIMD (96 VGPRs, 52-84 B spilled) 53.4 / 58.5 ms vs 4 waves 55.9 / 62.5 ms
-// (16-PAM at 13 / 25 dB, 4096 frames), 4-PAM 14.5 ms either way; 3 waves 55.6 / 62.0 ms.
-#define QR_DEMAP_WAVES 5
-#endif
+// Occupancy floor of the per-symbol kernel: 5 waves/SIMD (96 VGPRs, 52-84 B spilled) 53.4 / 58.5 ms
+// vs 4 waves 55.9 / 62.5 ms (16-PAM at 13 / 25 dB, 4096 frames), 4-PAM 14.5 ms either way.
+constexpr int kDemapWaves = 5;
 template <bool FAST, int BPS>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QR_DEMAP_WAVES, 8))) k_demap(const DemapTables *__restrict__ tab, const MathTables *__restrict__ gmt,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kDemapWaves, 8))) k_demap(const DemapTables *__restrict__ tab, const MathTables *__restrict__ gmt,
                                                int B, int ld, int64_t S, const double *__restrict__ n,
                                                const int64_t *__restrict__ j, double alpha,
                                                double *__restrict__ lappr) {
@@ -60,35 +59,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QR_DEM
 }
 
 // ---------------------------------------------------------------------------
-// Hypothesis-parallel demapper (default for 2..64-PAM on 64-frame tiles).
-//
-// One workgroup = one symbol position s x 64 frames, W = min(M, 4) wavefronts; wave w
-// takes the hypotheses i = w, w + W, ... (the reference's loop over i,
-// noisemapper.pyx:490-530), lane = frame.  Per (frame, i) a lane runs the root search
-// for y_i (g_inv_search, :310-345, fast path), the M-term sum S_i in the reference's order
-// (:503-515) and parks q_i = dF[i] / S_i in LDS; after a barrier, wave k % W combines
-// bit k of every frame: N[k] / D[k] accumulated over i ascending (:521-530, per k exactly
-// the reference's sequence of additions), log(N) - log(D) (:534-538), times alpha.
-// The root search's certified closed form needs at most one exact F_Y per (frame, i),
-// for ~2 % of the lanes; instead of the wave running a divergent M-erf F_Y whenever any
-// of its lanes needs one, the lanes' evaluation points are compacted into LDS (ballot +
-// mbcnt) and the wave evaluates their M erf terms with one lane per (point, m), 64 / M
-// points per pass, after which each owner sums its M terms in m order (noisemapper.pyx:
-// 278-286: the same products, the same sequence of additions).  Per lane the state is
-// one search and one sum (no M-long accumulators): no scratch spill.
-// The grid strides over the (s, tile) items, so the 4 KiB of glibc tables are staged once
-// per resident workgroup.
-constexpr int kDemapHypWaves = 4;
-constexpr int kDemapHypMaxBps = 6;
-#ifndef QR_DEMAP_EXPW
-#define QR_DEMAP_EXPW 1      // LLR-sum exp: glibc main path branch-free, specials per wave (g_exp_wave)
-#endif
-#ifndef QR_DEMAP_HYP_UNROLL
-#define QR_DEMAP_HYP_UNROLL 4
-#endif
-#ifndef QR_DEMAP_HYP_EU
-#define QR_DEMAP_HYP_EU 1    // amdgpu_waves_per_eu floor of k_demap_hyp (1 = the compiler's choice)
-#endif
+// Root search of the 64-frame-tile demapper (k_demap_wave, below).  The certified closed form
+// of the search needs at most one exact F_Y per (frame, hypothesis), for ~2 % of the lanes;
+// instead of the wave running a divergent M-erf F_Y whenever any of its lanes needs one, the
+// lanes' evaluation points are compacted into LDS (ballot + mbcnt) and the wave evaluates
+// their M erf terms with one lane per (point, m), 64 / M points per pass, after which each
+// owner sums its M terms in m order (noisemapper.pyx:278-286: the same products, the same
+// sequence of additions).
+constexpr int kDemapWaveMaxBps = 6;
+// LLR-sum loop unroll of k_demap_wave (1 / 16: 50.3 / 57.0 ms vs 46.8 at 4, 16-PAM, round 3)
+constexpr int kDemapUnroll = 4;
 
 // rank of this lane among the set lanes of mk below it
 __device__ __forceinline__ int lane_rank(uint64_t mk) {
@@ -139,86 +119,9 @@ __device__ __forceinline__ double g_inv_search_wave(const DemapTables &t, const 
     return search_replay(cmp);   // no certified window / outside the closed form (rare): per lane
 }
 
-template <int BPS>
-__global__ void __launch_bounds__(64 * kDemapHypWaves) __attribute__((amdgpu_waves_per_eu(QR_DEMAP_HYP_EU, 8)))
-k_demap_hyp(const DemapTables *__restrict__ tab,
-                                                                  const MathTables *__restrict__ gmt, int B, int ld,
-                                                                  int64_t S, const double *__restrict__ n,
-                                                                  const int64_t *__restrict__ j, double alpha,
-                                                                  double *__restrict__ lappr) {
-    constexpr int M = 1 << BPS;
-    constexpr int W = M < kDemapHypWaves ? M : kDemapHypWaves;
-    constexpr int HPW = M / W;
-    __shared__ GlibcExpLog gt;
-    __shared__ double q[M][64];
-    __shared__ double ey[W][64], et[W][64];
-    stage_glibc_exp_log(&gt, &kGlibcConst);
-    const DemapTables &t = *tab;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t tiles = ld / 64;
-    const int64_t items = S * tiles;
-    for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {   // uniform per workgroup
-        const int64_t s = it / tiles;
-        const int f = (int)(it - s * tiles) * 64 + lane;
-        const bool valid = f < B;
-        const double nv = valid ? n[s * ld + f] : 0.5;   // padding lanes: a harmless target
-        const int64_t jv = valid ? j[s * ld + f] : 0;
-        const bool jok = jv >= 0 && jv < M;
-        const int jj = jok ? (int)jv : 0;
-        const double aj = t.a[jj];
-#pragma unroll 1
-        for (int h = 0; h < HPW; ++h) {
-            const int i = w + h * W;
-#if defined(QR_EXPERIMENT_NO_SEARCH)   // cost breakdown only (wrong results): the start point
-            const double y = quantile_start(t, i, search_target(t, nv, i));
-#elif defined(QR_EXPERIMENT_NEWTON_ONLY)   // cost breakdown only: start + Newton, no bracket/bisection
-            double y = 0, Wd = 0;
-            newton_root(t, *gmt, search_target(t, nv, i), i, y, Wd);
-#else
-            const double y = g_inv_search_wave<M>(t, *gmt, nv, i, ey[w], et[w], lane);
-#endif
-            // noisemapper.pyx:503-515 in the reference's summation order (k < j, p[j], k > j)
-            // as one loop with the argument selected per lane (see demap_symbol)
-            double sum = 0;
-#pragma unroll QR_DEMAP_HYP_UNROLL
-            for (int k = 0; k < M; ++k) {
-#ifdef QR_EXPERIMENT_NO_LLR   // cost breakdown only (wrong results)
-                sum += y * t.p[k];
-                continue;
-#endif
-                const double e = (2 * y - t.a[k] - aj) * (t.a[k] - aj);
-                // (k == j: the term is p[j]; its exp argument, 0, would send the wave down the
-                // special-case path of g_exp_wave for nothing)
-                const double arg = k < jj ? e : k == jj ? 1.0 : div_two_s2(t, e);
-#if QR_DEMAP_EXPW
-                const double ex = g_exp_wave(arg, gt);
-#else
-                const double ex = g_exp_full(arg, gt);
-#endif
-                const double term = k == jj ? t.p[jj] : ex * t.p[k];
-                sum += term;
-            }
-            q[i][lane] = t.dF[i] / sum;
-        }
-        __syncthreads();
-        for (int k = w; k < BPS; k += W) {
-            double N = 0, D = 0;
-#pragma unroll
-            for (int i = 0; i < M; ++i) {   // noisemapper.pyx:521-530: Gray bit k of i
-                const int mi = i >> k;
-                if ((mi * (mi + 1)) & 3) D += q[i][lane];
-                else                     N += q[i][lane];
-            }
-            const double out = (g_log_full(N, gt) - g_log_full(D, gt)) * alpha;   // :534-538, x alpha
-            if (valid) lappr[(s * BPS + k) * ld + f] = jok ? out : __builtin_nan("");
-        }
-        __syncthreads();   // q is rewritten by the next item
-    }
-}
-
 // ---------------------------------------------------------------------------
-// Wave-private demapper (knob demap_hyp = 3): the same per-(frame, hypothesis) work as
-// k_demap_hyp, but ONE wave walks all M hypotheses of its own 64-frame tile (lane = frame) and
+// Wave-private demapper (knob demap_hyp = 1, the default): ONE wave walks all M hypotheses of its
+// own 64-frame tile (lane = frame; the reference's loop over i, noisemapper.pyx:490-530) and
 // keeps the Gray-labelled sums N[k] / D[k] of its lanes in a wave-private LDS slice, updated
 // in i order (noisemapper.pyx:521-530: per bit the reference's sequence of additions).  No
 // workgroup barrier: a wave's search lengths never hold up another wave.  The exact F_Y of the
@@ -254,7 +157,7 @@ __global__ void __launch_bounds__(256) k_demap_wave(const DemapTables *__restric
             const double y = g_inv_search_wave<M>(t, *gmt, nv, i, ey[w], et[w], lane);
             // noisemapper.pyx:503-515 in the reference's summation order (k < j, p[j], k > j)
             double sum = 0;
-#pragma unroll QR_DEMAP_HYP_UNROLL
+#pragma unroll kDemapUnroll
             for (int k = 0; k < M; ++k) {
                 const double e = (2 * y - t.a[k] - aj) * (t.a[k] - aj);
                 const double arg = k < jj ? e : k == jj ? 1.0 : div_two_s2(t, e);
@@ -291,7 +194,7 @@ static bool launch_demap_wave(int bps, unsigned grid, hipStream_t st, const qr_d
 }
 
 // workgroups of the grid-stride demap: enough to fill every CU several times over
-static unsigned demap_hyp_grid(int device, int64_t items) {
+static unsigned demap_wave_grid(int device, int64_t items) {
     static std::atomic<int> cus[64];
     int cu = (device >= 0 && device < 64) ? cus[device].load() : 0;
     if (cu <= 0) {
@@ -301,18 +204,6 @@ static unsigned demap_hyp_grid(int device, int64_t items) {
     }
     const int64_t want = (int64_t)cu * 16;
     return (unsigned)(items < want ? items : want);
-}
-
-static bool launch_demap_hyp(int bps, unsigned grid, hipStream_t st, const qr_demap *dm, int B, int ld, int64_t S,
-                             const double *n, const int64_t *j, double alpha, double *lappr) {
-    switch (bps) {
-#define QR_DEMAP_HYP(b) \
-        case b: k_demap_hyp<b><<<grid, 64 * (((1 << b) < kDemapHypWaves) ? (1 << b) : kDemapHypWaves), 0, st>>>( \
-            dm->d_tables, dm->d_mtab, B, ld, S, n, j, alpha, lappr); return true;
-        QR_DEMAP_HYP(1) QR_DEMAP_HYP(2) QR_DEMAP_HYP(3) QR_DEMAP_HYP(4) QR_DEMAP_HYP(5) QR_DEMAP_HYP(6)
-#undef QR_DEMAP_HYP
-        default: return false;
-    }
 }
 
 template <int BPS>
@@ -534,12 +425,10 @@ int demap_batch_device(const qr_demap *dm, int B, int ld, int64_t S, const doubl
     ProfScope ps("demap", s);
     const bool fast = g_demap_fast.load() != 0;
     const int hyp = g_demap_hyp.load();
-    if (fast && (hyp >= 2 || (hyp == 1 && dm->h.bps >= kDemapHypAutoBps)) && ld % kWave == 0 &&
-        dm->h.bps <= kDemapHypMaxBps) {
+    if (fast && hyp >= 1 && ld % kWave == 0 &&
+        dm->h.bps <= kDemapWaveMaxBps) {
         const int64_t items = S * (ld / kWave);
-        if (hyp == 3) launch_demap_wave(dm->h.bps, demap_hyp_grid(dm->device, (items + 3) / 4), s, dm, B, ld, S, n, j,
-                                        alpha, lappr);
-        else launch_demap_hyp(dm->h.bps, demap_hyp_grid(dm->device, items), s, dm, B, ld, S, n, j, alpha, lappr);
+        launch_demap_wave(dm->h.bps, demap_wave_grid(dm->device, (items + 3) / 4), s, dm, B, ld, S, n, j, alpha, lappr);
     } else {
         const int64_t items = S * ld;
         launch_demap_bps(dm->h.bps, fast, (unsigned)((items + 255) / 256), s, dm, B, ld, S, n, j, alpha, lappr);

@@ -100,6 +100,8 @@ def load():
         pass
     L = C.CDLL(LIB_PATH)
     for name, args in SIGNATURES.items():
+        if os.environ.get("QAMR_LIB") and not hasattr(L, name):
+            continue  # an experiment build of an older interface (scripts/exp_*): only what it exports
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = _RESTYPE.get(name, C.c_int)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B of the demapper kernels on the GPU at the bench's batch (B = 4096 frames, N = 64800):
-demap_hyp = 3 (wave-private: one wave walks all hypotheses of its tile), 2 (hypothesis-parallel,
-LDS combine), 0 (one lane per symbol), all with the fast root search: ms per launch (hipEvents,
+demap_hyp = 1 (wave-private: one wave walks all hypotheses of its tile; default), 0 (one lane per
+symbol), both with the fast root search: ms per launch (hipEvents,
 median of reps) and bit-identity of the LAPPRs.
     python scripts/demap_ab.py [--batch 4096] [--reps 3] [--variants 3,2,0]"""
 import argparse
@@ -17,7 +17,7 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cases", default="2:3.0,4:13.0,4:14.5,4:25.0")
-    ap.add_argument("--variants", default="3,2,0")
+    ap.add_argument("--variants", default="1,0")
     args = ap.parse_args()
     import torch
     import qamr
