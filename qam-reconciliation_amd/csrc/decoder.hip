@@ -495,7 +495,7 @@ struct IterArgs {
     const uint8_t *unsat_s;  // row t-2 (status to apply), or null
     uint8_t *unsat_p;        // row t-1 (parity of post(t-1)), or null at t = 1
     int32_t status_iter;     // t - 2
-    int ld;
+    int ld, f_off;           // the launch sweeps frames [f_off, f_off + gridDim.y * ft)
     Geom g;
     unsigned nbx;
     const GlibcTables *gglibc;
@@ -510,7 +510,7 @@ __device__ __forceinline__ void iter_block(const IterArgs &a, unsigned bx, unsig
     const int ft = 1 << a.g.lft;
     const int nsub = 256 >> a.g.lft;
     const int ld = a.ld;
-    const int f = (int)(by << a.g.lft) + (threadIdx.x & (ft - 1));
+    const int f = a.f_off + (int)(by << a.g.lft) + (threadIdx.x & (ft - 1));
     const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> a.g.lft);
     const bool was = a.active[f] != 0;
     const bool act = was && (!a.unsat_s || a.unsat_s[f] != 0);
@@ -805,7 +805,7 @@ static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
 struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3}, math{kStrict}, eps_max{40},
         lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024}, var_pace{28},
-        check_tail{4}, fused_iter{1};
+        check_tail{4}, fused_iter{1}, iter_streams{2};
 };
 static Tuning g_tune;
 
@@ -1232,7 +1232,10 @@ static int run_split2(const Plan &P, int max_it) {
 }
 
 // The one-launch-per-iteration schedule of small codes (k_iter): P(1) .. P(max_it + 1), the last
-// one the final parity sweep.
+// one the final parity sweep.  Knob iter_streams (default 2): the frames are cut into that many
+// ranges, each an independent chain of launches on its own stream (frames never depend on other
+// frames), so one range's gathers overlap another range's arithmetic instead of every launch
+// running a load phase then a compute phase.
 static int run_iter(const Plan &P, int max_it) {
     const DegreeClass &cls = P.code->classes[0];
     const int ld = P.ld;
@@ -1257,25 +1260,45 @@ static int run_iter(const Plan &P, int max_it) {
     a.nbx = (unsigned)((cls.n + per_block - 1) / per_block);
     a.gglibc = P.code->d_gtab;
     a.finite = P.w.acount + 2;
-    const dim3 grid(a.nbx, (unsigned)(ld >> a.g.lft));
     double *buf[2] = {P.w.c2v, P.w.c2v2};
+    const int tiles = ld >> a.g.lft;
+    const int nst = std::max(1, std::min({g_tune.iter_streams.load(), 2, tiles}));
+    const qr_code *code = P.code;
+    std::unique_lock<std::mutex> lk(code->mu, std::defer_lock);
+    hipStream_t st[2] = {P.s, P.s};
+    if (nst == 2) {
+        lk.lock();
+        if (int rc0 = side_stream(code, &st[1])) return rc0;
+        QR_HIP(hipEventRecord(code->ev[0], P.s));
+        QR_HIP(hipStreamWaitEvent(st[1], code->ev[0], 0));
+    }
+    // enqueue order interleaves the ranges; each stream runs its own chain
     for (int t = 1; t <= max_it + 1; ++t) {
         a.c2v_in = t == 1 ? nullptr : buf[(t - 1) & 1];
         a.c2v_out = t <= max_it ? buf[t & 1] : nullptr;
         a.unsat_s = t >= 3 ? P.w.unsat + (size_t)(t - 2) * ld : nullptr;
         a.unsat_p = t >= 2 ? P.w.unsat + (size_t)(t - 1) * ld : nullptr;
         a.status_iter = t - 2;
-        ProfScope ps(profiling_on() ? "iter_d" + std::to_string(cls.degree) : std::string(), P.s);
+        for (int r = 0; r < nst; ++r) {
+            const int t0 = tiles * r / nst, t1 = tiles * (r + 1) / nst;
+            a.f_off = t0 << a.g.lft;
+            const dim3 grid(a.nbx, (unsigned)(t1 - t0));
+            ProfScope ps(profiling_on() ? "iter_d" + std::to_string(cls.degree) : std::string(), st[r]);
 #define QR_CASE(DD)                                                                     \
     case DD:                                                                            \
-        k_iter<DD><<<grid, 256, 0, P.s>>>(a);                                           \
+        k_iter<DD><<<grid, 256, 0, st[r]>>>(a);                                         \
         break;
-        switch (cls.degree) {
-            QR_CASE(2) QR_CASE(3) QR_CASE(4) QR_CASE(5) QR_CASE(6) QR_CASE(7) QR_CASE(8) QR_CASE(9) QR_CASE(10)
-            default: return set_error(QR_EVALUE, "decode: no fused-iteration kernel for degree %d", cls.degree);
-        }
+            switch (cls.degree) {
+                QR_CASE(2) QR_CASE(3) QR_CASE(4) QR_CASE(5) QR_CASE(6) QR_CASE(7) QR_CASE(8) QR_CASE(9) QR_CASE(10)
+                default: return set_error(QR_EVALUE, "decode: no fused-iteration kernel for degree %d", cls.degree);
+            }
 #undef QR_CASE
-        QR_LAUNCH_CHECK();
+            QR_LAUNCH_CHECK();
+        }
+    }
+    if (nst == 2) {  // join: the final status follows both chains
+        QR_HIP(hipEventRecord(code->ev[4], st[1]));
+        QR_HIP(hipStreamWaitEvent(P.s, code->ev[4], 0));
     }
     return QR_OK;
 }
@@ -1533,7 +1556,7 @@ static std::atomic<int> *tune_knob(const char *name) {
         {"demap_hyp", &g_demap_hyp},        {"min_blocks", &g_tune.min_blocks},
         {"split_min_blocks", &g_tune.split_min_blocks},
         {"var_pace", &g_tune.var_pace},     {"check_tail", &g_tune.check_tail},
-        {"fused_iter", &g_tune.fused_iter},
+        {"fused_iter", &g_tune.fused_iter}, {"iter_streams", &g_tune.iter_streams},
     };
     const std::string n = name ? name : "";
     for (const auto &k : knobs)

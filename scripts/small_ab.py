@@ -14,7 +14,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1024)
-    ap.add_argument("--knobs", default="fused_iter=1;fused_iter=0")
+    ap.add_argument("--knobs", default="fused_iter=1,iter_streams=2;fused_iter=1,iter_streams=1;fused_iter=0")
     args = ap.parse_args()
     import torch
     import qamr

@@ -228,21 +228,27 @@ def test_fused_iteration_schedule_vs_oracle(gpu, code):
     llr[9, 3] = -0.0
     L = torch.from_numpy(llr.T.copy()).cuda()
     S = torch.from_numpy(synd.T.copy()).cuda()
-    saved = _lib.tune_get("fused_iter")
+    saved = {k: _lib.tune_get(k) for k in ("fused_iter", "iter_streams")}
     try:
         for mi in (1, 2, 3, 50):
             outs = []
-            for fi in (1, 0):   # one launch per iteration, the three-launch flat schedule
+            # one launch per iteration on two independent frame ranges / on one stream, then the
+            # three-launch flat schedule
+            for fi, ns in ((1, 2), (1, 1), (0, 1)):
                 _lib.tune_set("fused_iter", fi)
+                _lib.tune_set("iter_streams", ns)
                 outs.append([x.clone() for x in dec.decode_device(L, S, B, mi)])
                 torch.cuda.synchronize()
-            (f1, s1, i1), (f0, s0, i0) = outs
-            assert torch.equal(s1, s0) and torch.equal(i1, i0), mi
-            assert torch.equal(f1[:, :B].view(torch.int64), f0[:, :B].view(torch.int64)), mi
+            (f0, s0, i0) = outs[-1]
+            for f1, s1, i1 in outs[:-1]:
+                assert torch.equal(s1, s0) and torch.equal(i1, i0), mi
+                assert torch.equal(f1[:, :B].view(torch.int64), f0[:, :B].view(torch.int64)), mi
+            f1, s1, i1 = outs[0]
             s2, i2, fo = orc.decode_batch(llr, synd, mi)
             assert np.array_equal(s1.cpu().numpy(), s2) and np.array_equal(i1.cpu().numpy(), i2), mi
             assert_bit_exact(f1[:, :B].cpu().numpy().T, fo)
             if mi == 50:
                 assert 0 < s2.sum() < B and (i2[:8] == 0).all() and s2[:8].all()
     finally:
-        _lib.tune_set("fused_iter", saved)
+        for k, v in saved.items():
+            _lib.tune_set(k, v)
