@@ -168,6 +168,7 @@ struct VarArgs {
     const int32_t *alist, *acount;  // as CheckArgs
     unsigned nby;  // frame tiles (grid-stride launches)
     int gs;        // 1: a capped 1-D grid walks the nbx x nby tiles (the paced sweeps of run_split2, knob var_pace)
+    int boost;     // gs grid = boost x the paced width; as the live frame tiles drop to nby / k, min(k, boost) widths sweep
     // INIT sweep only: the strict arithmetic's finite flag (see kPackMaxDeg) is cleared when an
     // input LAPPR of a frame < fin_B is not below fin_bound in magnitude (null: not computed)
     int32_t *finite;
@@ -299,7 +300,9 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
     // Waves whose 64 frames all stopped leave; in a partly stopped wave the stopped
     // lanes run along (no divergent exit, so the loop state stays scalar): their
     // messages are never read again and their posteriors (the output) are not touched.
-    const bool act = a.active[f] != 0;
+    // Lanes past the compacted count (repeating the last listed frame) count as stopped:
+    // once fewer than a tile's frames remain, the tile's empty waves leave at once.
+    const bool act = live && a.active[f] != 0;
     if (!wave_any(act)) return;
     int64_t ci = (int64_t)bx * per * nsub + sub;
     if (ci >= a.n_checks) return;
@@ -453,8 +456,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
 template <bool INIT, bool NT>
 __global__ void __launch_bounds__(256) k_var(VarArgs a) {
     if (a.gs) {  // capped grid: tile t = (bx fastest, by), the grid's blocks sweep a moving window
-        const unsigned n = a.nbx * a.nby;
-        for (unsigned t = blockIdx.x; t < n; t += gridDim.x) {
+        unsigned ny = a.nby, stride = gridDim.x;
+        if (a.boost > 1) {
+            // The pacing spreads a full sweep over the concurrent check launch; once most frames
+            // have stopped, both launches shrink and a paced sweep of the few live tiles would be
+            // latency-bound (a few workgroups per CU walking many blocks each): widen it.
+            const unsigned w = gridDim.x / (unsigned)a.boost;
+            unsigned live = a.nby;
+            if (a.acount) live = min(a.nby, (unsigned)((*a.acount + (1 << a.g.lft) - 1) >> a.g.lft));
+            const unsigned m = live ? min((unsigned)a.boost, max(1u, a.nby / live)) : 1u;
+            stride = w * m;
+            ny = live;
+            if (blockIdx.x >= stride) return;
+        }
+        const unsigned n = a.nbx * ny;
+        for (unsigned t = blockIdx.x; t < n; t += stride) {
             const unsigned by = t / a.nbx, bx = t - by * a.nbx;
             if (frames_block_live(a.acount, by, a.g.lft)) var_block<INIT, NT>(a, bx, by);
         }
@@ -567,6 +583,155 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
     if (a.c2v_out) stage_glibc_tables(&tab, a.gglibc);
     if (a.finite && sld(a.finite)) iter_block<D, true>(a, blockIdx.x, blockIdx.y, tab, hb);
     else iter_block<D, false>(a, blockIdx.x, blockIdx.y, tab, hb);
+}
+
+// ---------------------------------------------------------------------------------------
+// Small codes, frame-resident (knob resident, default 1): ONE launch per decode, one
+// workgroup per frame for all its iterations, the frame's messages and posteriors in LDS
+// (configs[1], reg-(3,6) N=1008: 24 KiB of c2v + 8 KiB of posteriors).  Lane = check in the
+// check phase (check c's messages at slots D c .. D c + D - 1: single-degree codes only) and
+// lane = variable in the variable phase; each message and posterior is the same operation on
+// the same operands as in the frame-parallel kernels (only which lane evaluates it changes),
+// so the bits are the reference's.  Per frame the order is decoder.pyx:400-436's:
+//   post(0) = lappr (+ 0.0 on connected variables), parity -> stop with (1, 0) and the input;
+//   t = 1..max_it: check phase c2v(t) from post(t-1) (+ parity of post(t-1) for t >= 2 ->
+//   stop with (1, t-1) and post(t-1)); variable phase post(t) = lappr + sum c2v(t) in
+//   ascending edge order;  then parity of post(max_it) -> (1 or 0, max_it).
+// A frame stops on its own iteration (no lock-step), no per-iteration launch, no HBM
+// traffic for the messages.  In LDS message (c, i) lives at i C + c, so the lanes of a check
+// phase (consecutive checks) touch consecutive doubles.  Workgroup b takes frame (b % 8) ceil(B / 8) + b / 8, so the frames
+// of one XCD are contiguous columns and their LAPPR sectors stay in that XCD's L2.
+constexpr int kResThreads = 512;
+constexpr int kResMaxIter = 10000;  // one launch runs every iteration: bound its length
+constexpr int kResStaticLds = (int)sizeof(GlibcTablesBP) + (kResThreads / 64) * kPackWaveDoubles * 8;
+
+struct ResArgs {
+    int C, V, B, ld, max_it;
+    const int32_t *chk_var;              // check CSR: check c's variables at D c .. D c + D - 1
+    const int32_t *var_ptr, *var_slot;   // per variable, its edges (ascending) as check-CSR slots
+    const double *lappr;
+    const uint8_t *synd;
+    double *post;
+    uint8_t *success;
+    int32_t *iters;
+    const GlibcTables *gglibc;
+    double fin_bound;  // |lappr| below it for every variable -> the finite clamp (0: never)
+};
+
+// parity of the posteriors in LDS (decoder.pyx:235-257): 1 iff some check of this thread fails
+template <int D>
+__device__ __forceinline__ uint32_t res_parity(const ResArgs &a, int f, const double *post) {
+    uint32_t bad = 0;
+    for (int c = threadIdx.x; c < a.C; c += kResThreads) {
+        uint32_t par = a.synd[(size_t)c * a.ld + f];
+#pragma unroll
+        for (int i = 0; i < D; ++i) par ^= (post[a.chk_var[c * D + i]] < 0.0) ? 1u : 0u;
+        bad |= (par == 1u) ? 1u : 0u;
+    }
+    return bad;
+}
+
+__device__ __forceinline__ void res_finish(const ResArgs &a, int f, const double *post, int ok, int32_t it) {
+    for (int v = threadIdx.x; v < a.V; v += kResThreads) a.post[(size_t)v * a.ld + f] = post[v];
+    if (threadIdx.x == 0) {
+        a.success[f] = (uint8_t)ok;
+        a.iters[f] = it;
+    }
+}
+
+template <int D, bool FIN>
+__device__ __forceinline__ void resident_loop(const ResArgs &a, int f, double *msg, double *post,
+                                              const GlibcTablesBP &tab, double *wb) {
+    const int tid = threadIdx.x;
+    const size_t ld = a.ld;
+    const auto K = Arith<kStrict>::regs();
+    // the first check of this thread (all of them when C <= kResThreads): its variables and
+    // syndrome bit stay in registers across the iterations (D <= 6: within 128 VGPRs; above,
+    // the indices would spill and are re-read from L1 instead)
+    constexpr bool kPre = D <= 6;
+    const int c_first = min(tid, a.C - 1);
+    int pv[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) pv[i] = kPre ? a.chk_var[c_first * D + i] : 0;
+    const uint8_t sb_first = a.synd[(size_t)c_first * ld + f];
+    for (int t = 1; t <= a.max_it; ++t) {
+        uint32_t bad = 0;
+        for (int c0 = 0; c0 < a.C; c0 += kResThreads) {
+            if (c0 + (tid & ~63) >= a.C) break;  // wave-uniform: no check left for this wave
+            const int c = c0 + tid;
+            const bool live = c < a.C;
+            const int cc = live ? c : a.C - 1;  // surplus lanes repeat the last check, store nothing
+            const uint8_t sb = c0 == 0 ? sb_first : a.synd[(size_t)cc * ld + f];
+            uint32_t par = sb;
+            double m[D];
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                const double p = post[(kPre && c0 == 0) ? pv[i] : a.chk_var[cc * D + i]];
+                par ^= (p < 0.0) ? 1u : 0u;     // decoder.pyx:243-246
+                m[i] = p - msg[i * a.C + cc];    // :296-297
+            }
+            if (live) bad |= (par == 1u) ? 1u : 0u;
+            double out[D];
+            check_strict_packed<D, FIN ? kClampFinite : kClampFull>(m, out, wb, tab, K);
+            const double s = sb ? -1.0 : 1.0;
+            if (live) {
+#pragma unroll
+                for (int i = 0; i < D; ++i) msg[i * a.C + cc] = s * out[i];  // only this lane reads them back
+            }
+        }
+        // the parity of post(t-1) (t = 1: post(0), whose parity is the input's, already tested)
+        const int any_bad = __syncthreads_or((int)bad);
+        if (t >= 2 && !any_bad) {  // decoder.pyx:431-433 at iteration t-1
+            res_finish(a, f, post, 1, t - 1);
+            return;
+        }
+        for (int v = tid; v < a.V; v += kResThreads) {  // decoder.pyx:285-298
+            double p = a.lappr[(size_t)v * ld + f];
+            const int b = a.var_ptr[v], e = a.var_ptr[v + 1];
+            for (int k = b; k < e; ++k) {
+                const int sl = a.var_slot[k], c = sl / D;
+                p += msg[(sl - c * D) * a.C + c];
+            }
+            post[v] = p;
+        }
+        __syncthreads();
+    }
+    const int any_bad = __syncthreads_or((int)res_parity<D>(a, f, post));
+    res_finish(a, f, post, any_bad ? 0 : 1, a.max_it);  // decoder.pyx:435-436
+}
+
+template <int D>
+__global__ void __launch_bounds__(kResThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) k_resident(ResArgs a) {
+    extern __shared__ double res_dyn[];
+    __shared__ GlibcTablesBP tab;
+    __shared__ double hb[(kResThreads / 64) * kPackWaveDoubles];
+    const int q = (a.B + 7) / 8;
+    const int f = (int)(blockIdx.x & 7u) * q + (int)(blockIdx.x >> 3);
+    if (f >= a.B) return;  // block-uniform
+    stage_glibc_tables(&tab, a.gglibc);
+    const int tid = threadIdx.x;
+    const size_t ld = a.ld;
+    double *msg = res_dyn, *post = res_dyn + (size_t)a.C * D;
+    for (int s = tid; s < a.C * D; s += kResThreads) msg[s] = 0.0;
+    bool small = true;
+    for (int v = tid; v < a.V; v += kResThreads) {  // decoder.pyx:408,420-421
+        const double x = a.lappr[(size_t)v * ld + f];
+        small &= __builtin_fabs(x) < a.fin_bound;
+        post[v] = (a.var_ptr[v + 1] > a.var_ptr[v]) ? x + 0.0 : x;
+    }
+    const int fin = __syncthreads_and((int)small);
+    // decoder.pyx:400-405: post(0) has the input's signs (only -0.0 -> +0.0 differs)
+    if (!__syncthreads_or((int)res_parity<D>(a, f, post))) {
+        for (int v = tid; v < a.V; v += kResThreads) a.post[(size_t)v * ld + f] = a.lappr[(size_t)v * ld + f];
+        if (tid == 0) {
+            a.success[f] = 1;
+            a.iters[f] = 0;
+        }
+        return;
+    }
+    double *wb = hb + (tid >> 6) * kPackWaveDoubles;
+    if (fin) resident_loop<D, true>(a, f, msg, post, tab, wb);
+    else resident_loop<D, false>(a, f, msg, post, tab, wb);
 }
 
 // One launch = the check sweep of one frame half and the variable sweep of the
@@ -805,7 +970,7 @@ static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
 struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3}, math{kStrict}, eps_max{40},
         lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024}, var_pace{28},
-        check_tail{4}, fused_iter{1}, iter_streams{2};
+        check_tail{4}, fused_iter{1}, iter_streams{2}, var_boost{4}, resident{1};
 };
 static Tuning g_tune;
 
@@ -891,6 +1056,7 @@ struct Plan {
         a.alist = a.acount = nullptr;
         a.nby = (unsigned)((f1 - f0) >> a.g.lft);
         a.gs = 0;
+        a.boost = 1;
         a.finite = nullptr;
         a.fin_bound = 0.0;
         a.fin_B = 0;
@@ -989,7 +1155,9 @@ static int launch_var(const Plan &P, int f0, int f1, int32_t *finite = nullptr, 
     const int64_t cap = (int64_t)P.var_pace * (((int64_t)a.nby << a.g.lft) / 128);  // per 128 frames
     if (cap > 0 && (int64_t)a.nbx * a.nby > cap) {
         a.gs = 1;
-        grid = dim3((unsigned)cap, 1);
+        // knob var_boost (default 4, 1 = off): the sweep widens as the live tiles drop
+        a.boost = std::max(1, std::min(g_tune.var_boost.load(), 16));
+        grid = dim3((unsigned)(cap * a.boost), 1);
     }
     if (P.nt) k_var<INIT, true><<<grid, 256, 0, P.s>>>(a);
     else k_var<INIT, false><<<grid, 256, 0, P.s>>>(a);
@@ -1303,6 +1471,53 @@ static int run_iter(const Plan &P, int max_it) {
     return QR_OK;
 }
 
+// The frame-resident decode (k_resident) runs a code whose messages and posteriors fit two
+// workgroups' LDS per CU (so 16 waves of <= 128 VGPRs per CU) under the strict arithmetic.
+static size_t resident_lds(const qr_code *code) { return (size_t)(code->E + code->V) * sizeof(double); }
+static bool resident_code(const qr_code *code) {
+    return g_tune.resident.load() && math_mode(kNormal) == kStrict && code->classes.size() == 1 &&
+           code->classes[0].degree >= 2 && code->classes[0].degree <= kPackMaxDeg &&
+           code->classes[0].n == code->C && code->C <= INT32_MAX / kPackMaxDeg && code->V < INT32_MAX &&
+           resident_lds(code) + kResStaticLds <= 80 * 1024;
+}
+
+static int run_resident(const qr_code *code, int B, int ld, const double *lappr, const uint8_t *synd, int max_it,
+                        double *final_post, uint8_t *success, int32_t *iters, hipStream_t s) {
+    ResArgs a;
+    a.C = (int)code->C;
+    a.V = (int)code->V;
+    a.B = B;
+    a.ld = ld;
+    a.max_it = max_it;
+    a.chk_var = code->d_chk_var;
+    a.var_ptr = code->d_var_ptr;
+    a.var_slot = code->d_var_slot;
+    a.lappr = lappr;
+    a.synd = synd;
+    a.post = final_post;
+    a.success = success;
+    a.iters = iters;
+    a.gglibc = code->d_gtab;
+    // the finite clamp's bound, as decode_batch_device's: 2^e, e = 1000 - (max_it + 2) log2(dv_max + 1)
+    const double fin_x = ((double)max_it + 2.0) * std::log2((double)code->max_dv + 1.0);
+    const int fin_e = fin_x > 999.0 ? 0 : 1000 - (int)std::ceil(fin_x);
+    a.fin_bound = fin_e >= 1 ? std::ldexp(1.0, fin_e) : 0.0;
+    const unsigned grid = (unsigned)(8 * ((B + 7) / 8));
+    const size_t lds = resident_lds(code);
+    ProfScope ps(profiling_on() ? "resident_d" + std::to_string(code->classes[0].degree) : std::string(), s);
+#define QR_CASE(DD)                                          \
+    case DD:                                                 \
+        k_resident<DD><<<grid, kResThreads, lds, s>>>(a);    \
+        break;
+    switch (code->classes[0].degree) {
+        QR_CASE(2) QR_CASE(3) QR_CASE(4) QR_CASE(5) QR_CASE(6) QR_CASE(7) QR_CASE(8) QR_CASE(9) QR_CASE(10)
+        default: return set_error(QR_EVALUE, "decode: no frame-resident kernel for degree %d", code->classes[0].degree);
+    }
+#undef QR_CASE
+    QR_LAUNCH_CHECK();
+    return QR_OK;
+}
+
 int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr, const uint8_t *synd, int max_it,
                         double *final_post, uint8_t *success, int32_t *iters, void *ws_ptr, size_t ws_size,
                         hipStream_t s) {
@@ -1313,6 +1528,8 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     if (ws_size < ws_bytes(code, ld, max_it))
         return set_error(QR_EVALUE, "decode: workspace too small (%zu < %zu)", ws_size, ws_bytes(code, ld, max_it));
     DeviceGuard dg(code->device);
+    if (max_it > 0 && max_it <= kResMaxIter && resident_code(code))
+        return run_resident(code, B, ld, lappr, synd, max_it, final_post, success, iters, s);
     Plan P{code, B, ld, lappr, synd, final_post, success, iters, carve(code, ld, max_it, ws_ptr), g_tune.nt.load() != 0, s};
     const int64_t rows = (int64_t)(max_it > 0 ? max_it : 0) + 2;  // no int overflow at INT_MAX
     int rc;
@@ -1446,6 +1663,7 @@ static int free_code(qr_code *c) {
     (void)hipFree(c->d_chk_var);
     (void)hipFree(c->d_var_ptr);
     (void)hipFree(c->d_var_edge);
+    (void)hipFree(c->d_var_slot);
     (void)hipFree(c->d_mtab);
     (void)hipFree(c->d_gtab);
     for (auto &e : c->ev)
@@ -1496,6 +1714,15 @@ int qr_code_create(const int64_t *e_to_v, const int64_t *e_to_c, int64_t nv, int
         (rc = upload(&code->d_var_edge, var_edge))) {
         free_code(code);
         return rc;
+    }
+    {
+        std::vector<int32_t> slot_of_edge((size_t)E), var_slot((size_t)E);
+        for (int64_t s = 0; s < E; ++s) slot_of_edge[(size_t)chk_edge[(size_t)s]] = (int32_t)s;
+        for (int64_t k = 0; k < E; ++k) var_slot[(size_t)k] = slot_of_edge[(size_t)var_edge[(size_t)k]];
+        if ((rc = upload(&code->d_var_slot, var_slot))) {
+            free_code(code);
+            return rc;
+        }
     }
     {
         std::vector<MathTables> mt(1);
@@ -1555,8 +1782,9 @@ static std::atomic<int> *tune_knob(const char *name) {
         {"side", &g_tune.side},             {"demap_fast", &g_demap_fast},
         {"demap_hyp", &g_demap_hyp},        {"min_blocks", &g_tune.min_blocks},
         {"split_min_blocks", &g_tune.split_min_blocks},
-        {"var_pace", &g_tune.var_pace},     {"check_tail", &g_tune.check_tail},
+        {"var_pace", &g_tune.var_pace},     {"check_tail", &g_tune.check_tail}, {"var_boost", &g_tune.var_boost},
         {"fused_iter", &g_tune.fused_iter}, {"iter_streams", &g_tune.iter_streams},
+        {"resident", &g_tune.resident},
     };
     const std::string n = name ? name : "";
     for (const auto &k : knobs)

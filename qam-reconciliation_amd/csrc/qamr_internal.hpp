@@ -96,6 +96,9 @@ struct qr_code {
     // per variable, edge ids ascending.
     int32_t *d_chk_ptr = nullptr, *d_chk_edge = nullptr, *d_chk_var = nullptr;
     int32_t *d_var_ptr = nullptr, *d_var_edge = nullptr;
+    // per variable, edges ascending as above, each given by its position in the check CSR
+    // (chk_ptr[c] + i): the frame-resident small-code decoder's message index
+    int32_t *d_var_slot = nullptr;
     std::vector<DegreeClass> classes;
     int64_t fb_rows = 0;  // rows of the F scratch (sum over runtime-degree classes)
     qr::MathTables *d_mtab = nullptr;  // box-plus exp/log tables (fastmath.hpp)

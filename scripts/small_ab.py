@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """configs[1] (reg-(3,6) N=1008, 4-PAM 3 dB, B = 1024, 50 iterations): decode time per batch
-with the one-launch-per-iteration schedule (fused_iter = 1) vs the flat three-launch schedule
-(fused_iter = 0), and bit-identity of the outputs.   python scripts/small_ab.py [--reps 20]"""
+with the frame-resident decode (resident = 1), the one-launch-per-iteration schedule
+(fused_iter = 1) and the flat three-launch schedule (fused_iter = 0), and bit-identity of the outputs.   python scripts/small_ab.py [--reps 20]"""
 import argparse
 import json
 import os
@@ -14,7 +14,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1024)
-    ap.add_argument("--knobs", default="fused_iter=1,iter_streams=2;fused_iter=1,iter_streams=1;fused_iter=0")
+    ap.add_argument("--knobs", default="resident=1;resident=0,fused_iter=1,iter_streams=2;"
+                    "resident=0,fused_iter=1,iter_streams=1;resident=0,fused_iter=0")
     args = ap.parse_args()
     import torch
     import qamr

@@ -201,7 +201,8 @@ def _check_regular_irregular_var(N, dc, seed):
 
 @pytest.mark.parametrize("code", ["reg1008", "irr_d4", "irr_d7", "irr_d10"])
 def test_fused_iteration_schedule_vs_oracle(gpu, code):
-    """Small codes decode with one launch per iteration (k_iter: posteriors summed on the fly
+    """Small codes decode in one frame-resident launch (k_resident: a workgroup per frame, its
+    messages in LDS) or with one launch per iteration (k_iter: posteriors summed on the fly
     from double-buffered messages, status folded in): bit-identical to the three-launch flat
     schedule (knob fused_iter = 0) and to the oracle, for max_iterations 1, 2, 3, 50, incl.
     frames that converge at iteration 0 (input already a codeword), +-inf / NaN / -0.0 LAPPRs."""
@@ -228,13 +229,14 @@ def test_fused_iteration_schedule_vs_oracle(gpu, code):
     llr[9, 3] = -0.0
     L = torch.from_numpy(llr.T.copy()).cuda()
     S = torch.from_numpy(synd.T.copy()).cuda()
-    saved = {k: _lib.tune_get(k) for k in ("fused_iter", "iter_streams")}
+    saved = {k: _lib.tune_get(k) for k in ("fused_iter", "iter_streams", "resident")}
     try:
         for mi in (1, 2, 3, 50):
             outs = []
-            # one launch per iteration on two independent frame ranges / on one stream, then the
-            # three-launch flat schedule
-            for fi, ns in ((1, 2), (1, 1), (0, 1)):
+            # one frame-resident launch per decode; one launch per iteration on two independent
+            # frame ranges / on one stream; then the three-launch flat schedule
+            for rs, fi, ns in ((1, 1, 2), (0, 1, 2), (0, 1, 1), (0, 0, 1)):
+                _lib.tune_set("resident", rs)
                 _lib.tune_set("fused_iter", fi)
                 _lib.tune_set("iter_streams", ns)
                 outs.append([x.clone() for x in dec.decode_device(L, S, B, mi)])

@@ -77,7 +77,8 @@ TUNINGS = [dict(split=1), dict(split=2, check_per=1), dict(check_ft=64, check_pe
            dict(side=0, compact=0), dict(min_blocks=0), dict(min_blocks=4096, split=1),
            dict(split_min_blocks=4096), dict(split_min_blocks=0, min_blocks=0),
            dict(var_pace=0), dict(var_pace=3, var_per=1, compact=0), dict(var_pace=4096),
-           dict(check_tail=0), dict(check_tail=3, check_per=7, compact=0), dict(check_tail=2, split=1)]
+           dict(check_tail=0), dict(check_tail=3, check_per=7, compact=0), dict(check_tail=2, split=1),
+           dict(var_boost=1), dict(var_boost=16, var_pace=3, var_per=1)]
 
 
 def test_schedule_and_tuning_invariance(gpu):
@@ -86,7 +87,7 @@ def test_schedule_and_tuning_invariance(gpu):
 
     _, _, dec, pipe, batch, lappr = _dvbs2_batch(320, 3.6, seed=1)
     names = ["split", "check_ft", "check_per", "var_ft", "var_per", "nt", "lds_pad_kb", "compact", "side", "min_blocks",
-             "split_min_blocks", "var_pace", "check_tail"]
+             "split_min_blocks", "var_pace", "check_tail", "var_boost"]
     saved = {k: _lib.tune_get(k) for k in names}
     try:
         ref = [x.clone() for x in dec.decode_device(lappr, batch.synd, batch.B, 50)]
