@@ -340,7 +340,7 @@ def kernel_stats():
 
     out = {}
     for k in ("check", "check_d7", "check_d6", "check1", "fused_d7", "var", "var_init", "parity", "status", "demap",
-              "iter_d6"):
+              "iter_d6", "resident_d6"):
         ms, n = qamr.profile_query(k)
         if n:
             out[k] = {"avg_us": 1e3 * ms / n, "launches": n, "total_ms": ms}
