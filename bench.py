@@ -65,7 +65,7 @@ PRICED = ("check_d7", "fused_d7", "demap")
 
 # (name, workload, snr, batch, steps, BASELINE.json config it measures)
 SECONDARY = [
-    ("configs1_reg1008_4pam", "reg1008_4pam", 3.0, 1024, 5, "configs[1]: reg-(3,6) N=1008, 4-PAM, B=1024"),
+    ("configs1_reg1008_4pam", "reg1008_4pam", 3.0, 1024, 50, "configs[1]: reg-(3,6) N=1008, 4-PAM, B=1024"),
     ("configs3_dvbs2_16pam", "dvbs2_16pam", 13.0, 4096, 3,
      "configs[3]: N=64800 16-PAM, demap fused into the step, B=4096, 13 dB (all 50 iterations)"),
     ("op_dvbs2_4pam_4.0dB", "dvbs2_4pam", 4.0, 4096, 3,

@@ -50,7 +50,7 @@ def main():
         names = sorted({c for k in ctr.values() for c in k})
         lines.append("\n| kernel | " + " | ".join(names) + " |\n|---|" + "---|" * len(names))
         for k, cs in sorted(ctr.items(), key=lambda kv: -max((sum(v) / len(v) for v in kv[1].values()), default=0)):
-            if not any(x in k for x in ("k_fused", "k_check", "k_var", "k_demap", "k_bob")):
+            if not any(x in k for x in ("k_fused", "k_check", "k_var", "k_demap", "k_bob", "k_resident", "k_iter")):
                 continue
             vals = [f"{sum(cs[n]) / len(cs[n]):.4g}" if cs.get(n) else "" for n in names]
             lines.append(f"| `{k}` | " + " | ".join(vals) + " |")

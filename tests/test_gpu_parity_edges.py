@@ -254,3 +254,47 @@ def test_fused_iteration_schedule_vs_oracle(gpu, code):
     finally:
         for k, v in saved.items():
             _lib.tune_set(k, v)
+
+
+@pytest.mark.parametrize("B", [1, 7, 65, 600])
+def test_resident_batch_shapes_vs_oracle(gpu, B):
+    """The frame-resident decode (k_resident) at batch sizes that leave XCD slots empty
+    (workgroup b -> frame (b % 8) ceil(B / 8) + b / 8) and frames past a workgroup round:
+    every frame bit-exact against the oracle and the one-launch-per-iteration path, and the
+    padding columns of the output left untouched."""
+    import torch
+    import qamr
+    from qamr import _lib, codes
+    from qamr.pipeline import leading_dim
+
+    vid, cid = codes.regular_code(1008)
+    dec = qamr.Decoder(vid, cid)
+    orc = O.OracleCode(vid, cid)
+    V = dec.vnum
+    rng = np.random.default_rng(100 + B)
+    word = rng.integers(0, 2, (B, V)).astype(np.uint8)
+    synd = np.stack([orc.eval_syndrome(w) for w in word])
+    sig = rng.uniform(0.45, 0.8, B)[:, None]
+    llr = 2 / sig ** 2 * ((1 - 2.0 * word) + sig * rng.standard_normal((B, V)))
+    ld = leading_dim(B)
+    L = torch.zeros((V, ld), dtype=torch.float64, device="cuda")
+    L[:, :B] = torch.from_numpy(llr.T.copy()).cuda()
+    S = torch.zeros((dec.cnum, ld), dtype=torch.uint8, device="cuda")
+    S[:, :B] = torch.from_numpy(synd.T.copy()).cuda()
+    saved = _lib.tune_get("resident")
+    try:
+        outs = []
+        for rs in (1, 0):
+            _lib.tune_set("resident", rs)
+            fin = torch.full((V, ld), 7.0, dtype=torch.float64, device="cuda")
+            outs.append([x.clone() for x in dec.decode_device(L, S, B, 30, final_fi=fin)])
+            torch.cuda.synchronize()
+    finally:
+        _lib.tune_set("resident", saved)
+    (f1, s1, i1), (f0, s0, i0) = outs
+    assert torch.equal(s1, s0) and torch.equal(i1, i0)
+    assert torch.equal(f1[:, :B].view(torch.int64), f0[:, :B].view(torch.int64))
+    assert bool((f1[:, B:] == 7.0).all())
+    s2, i2, fo = orc.decode_batch(llr, synd, 30)
+    assert np.array_equal(s1.cpu().numpy(), s2) and np.array_equal(i1.cpu().numpy(), i2)
+    assert_bit_exact(f1[:, :B].cpu().numpy().T, fo)
