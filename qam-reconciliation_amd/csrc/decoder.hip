@@ -864,17 +864,20 @@ __global__ void k_init_status(int B, int ld, uint8_t *active, uint8_t *success, 
 // Frames in [f0, f1) whose posterior after sweep t satisfies the syndrome stop with
 // (success=1, iterations=t) (decoder.pyx:431-433, :402-405 for t = 0).  On the
 // final call every still-active frame stops with (0, max_iterations) (:435-436).
+// fid: the frame id of each column of a repacked range (null: column = frame).
 __global__ void k_status(int f0, int f1, int t, int final_call, int32_t final_iters,
-                         const uint8_t *__restrict__ unsat_t, uint8_t *active, uint8_t *success, int32_t *iters) {
+                         const uint8_t *__restrict__ unsat_t, uint8_t *active, uint8_t *success, int32_t *iters,
+                         const int32_t *__restrict__ fid) {
     const int f = f0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= f1 || !active[f]) return;
+    const int id = fid ? fid[f] : f;
     if (!unsat_t[f]) {
-        success[f] = 1;
-        iters[f] = t;
+        success[id] = 1;
+        iters[id] = t;
         active[f] = 0;
     } else if (final_call) {
-        success[f] = 0;
-        iters[f] = final_iters;
+        success[id] = 0;
+        iters[id] = final_iters;
         active[f] = 0;
     }
 }
@@ -884,11 +887,14 @@ __global__ void k_status(int f0, int f1, int t, int final_call, int32_t final_it
 // through LDS, one store per running frame.  STATUS: the status update of sweep t
 // (k_status, never the final call) is applied first, frame by frame, by the same thread:
 // one launch instead of two between the check sweeps of the two-stream schedule.
+// fid as k_status; hcount (or null): a host-mapped copy of the count, read by the host to
+// decide when to repack the range (run_split2).
 template <bool STATUS>
 __global__ void __launch_bounds__(1024) k_compact(int f0, int f1, uint8_t *__restrict__ active,
                                                   int32_t *__restrict__ list, int32_t *__restrict__ count, int t,
                                                   const uint8_t *__restrict__ unsat_t, uint8_t *__restrict__ success,
-                                                  int32_t *__restrict__ iters) {
+                                                  int32_t *__restrict__ iters, const int32_t *__restrict__ fid,
+                                                  int32_t *hcount) {
     __shared__ int wsum[16];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int base = 0;  // running count (every thread keeps the same value)
@@ -896,8 +902,9 @@ __global__ void __launch_bounds__(1024) k_compact(int f0, int f1, uint8_t *__res
         const int f = c0 + (int)threadIdx.x;
         bool a = f < f1 && active[f];
         if (STATUS && a && !unsat_t[f]) {  // k_status: satisfied -> (1, t), stops
-            success[f] = 1;
-            iters[f] = t;
+            const int id = fid ? fid[f] : f;
+            success[id] = 1;
+            iters[id] = t;
             active[f] = 0;
             a = false;
         }
@@ -913,7 +920,68 @@ __global__ void __launch_bounds__(1024) k_compact(int f0, int f1, uint8_t *__res
         base += tot;
         __syncthreads();  // wsum is rewritten by the next chunk
     }
-    if (threadIdx.x == 0) *count = base;
+    if (threadIdx.x == 0) {
+        *count = base;
+        if (hcount) *(volatile int32_t *)hcount = base;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Column repack of a converging frame range (run_split2, knob repack).  With the active-frame
+// lists a sweep's lanes map to the still-running frames, but those frames' columns lie
+// scattered over the range: once most frames have stopped, every 8-byte message access of a
+// lane is a cache line of its own, and a launch over a few hundred frames costs as much as one
+// over the whole range (MI355X, 4-PAM 4.0 dB: 3.7 ms for 418 running frames of 2048, 1.6 ms
+// for 76).  The repack moves the running frames' columns (messages, LAPPRs, syndrome bits) to
+// the front of a fresh buffer set, so the range shrinks and the lanes read contiguous columns
+// again; fid[] maps each column back to its frame for the status writes and the final posteriors.
+// Each column copy moves the same bits: the decode's arithmetic is untouched.
+
+// dst[r][f0 + p] = src[r][list[f0 + p]] for p < *count (rows r < rows), 8-byte elements
+__global__ void k_gather_cols64(int64_t rows, int f0, int ld, const int32_t *__restrict__ list,
+                                const int32_t *__restrict__ count, const double *__restrict__ src,
+                                double *__restrict__ dst) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= *count) return;
+    const int sc = list[f0 + p];
+    for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) dst[r * ld + f0 + p] = src[r * ld + sc];
+}
+__global__ void k_gather_cols8(int64_t rows, int f0, int ld, const int32_t *__restrict__ list,
+                               const int32_t *__restrict__ count, const uint8_t *__restrict__ src,
+                               uint8_t *__restrict__ dst) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= *count) return;
+    const int sc = list[f0 + p];
+    for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) dst[r * ld + f0 + p] = src[r * ld + sc];
+}
+// After the gathers: column f0 + p of the new set holds frame fid_src[list[f0 + p]] (p < count,
+// running) or nothing (count <= p < w: fid -1, stopped); the list becomes the identity.
+__global__ void k_repack_flags(int f0, int w, int32_t *__restrict__ list, const int32_t *__restrict__ count,
+                               const int32_t *__restrict__ fid_src, int32_t *__restrict__ fid_dst,
+                               uint8_t *__restrict__ active) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= w) return;
+    const int n = *count;
+    if (p < n) {
+        const int sc = list[f0 + p];
+        fid_dst[f0 + p] = fid_src ? fid_src[sc] : sc;
+        list[f0 + p] = f0 + p;
+        active[f0 + p] = 1;
+    } else {
+        fid_dst[f0 + p] = -1;
+        active[f0 + p] = 0;
+    }
+}
+// final_post[r][fid[q]] = post[r][q] for the columns q of [f0, f0 + w) holding a frame that is no
+// longer running (ALL: every column holding a frame -- the end of the decode)
+__global__ void k_scatter_post(int64_t rows, int f0, int w, int ld, const int32_t *__restrict__ fid,
+                               const uint8_t *__restrict__ active, int all, const double *__restrict__ post,
+                               double *__restrict__ final_post) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= w) return;
+    const int id = fid[f0 + q];
+    if (id < 0 || (!all && active[f0 + q])) return;
+    for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) final_post[r * ld + id] = post[r * ld + f0 + q];
 }
 
 // ------------------------------------------------------------------ launch
@@ -926,6 +994,14 @@ struct DecodeWs {
     int32_t *alist;  // active-frame lists of the frame ranges (ld entries)
     int32_t *acount; // their lengths: [0] range starting at frame 0, [1] the second half;
                      // [2] the finite flag of the input LAPPRs (first variable sweep)
+    // the two column sets a repacked frame range lives in (k_gather_cols*, run_split2); present
+    // when the caller's workspace has room for them (ws_bytes counts them when knob repack is on)
+    struct RepackSet {
+        double *c2v, *post, *lappr;
+        uint8_t *synd;
+        int32_t *fid;
+    } rs[2];
+    bool repack;
 };
 
 // Codes the one-launch-per-iteration schedule (k_iter) can run: one check-degree class of a
@@ -935,15 +1011,23 @@ static bool iter_code(const qr_code *code, int ld) {
            code->max_dv <= 64 && (size_t)code->E * ld * sizeof(double) <= ((size_t)1 << 30);
 }
 
-static size_t ws_bytes(const qr_code *code, int ld, int max_it) {
+static size_t ws_base_bytes(const qr_code *code, int ld, int max_it) {
     const int64_t rows = (int64_t)(max_it > 0 ? max_it : 0) + 2;  // no int overflow at INT_MAX
     const size_t msg = align_up((size_t)code->E * ld * sizeof(double), 256);
     return msg + (iter_code(code, ld) ? msg : 0) + align_up((size_t)ld, 256) +
            align_up((size_t)rows * ld, 256) + align_up((size_t)code->fb_rows * ld * sizeof(double), 256) +
            align_up((size_t)ld * sizeof(int32_t), 256) + 256;
 }
+static size_t repack_set_bytes(const qr_code *code, int ld) {
+    return align_up((size_t)code->E * ld * sizeof(double), 256) + 2 * align_up((size_t)code->V * ld * sizeof(double), 256) +
+           align_up((size_t)code->C * ld, 256) + align_up((size_t)ld * sizeof(int32_t), 256);
+}
+static size_t ws_repack_bytes(const qr_code *code, int ld);  // after g_tune
+static size_t ws_bytes(const qr_code *code, int ld, int max_it) {
+    return ws_base_bytes(code, ld, max_it) + ws_repack_bytes(code, ld);
+}
 
-static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
+static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base, size_t ws_size) {
     DecodeWs w;
     char *p = (char *)base;
     const int64_t rows = (int64_t)(max_it > 0 ? max_it : 0) + 2;  // no int overflow at INT_MAX
@@ -963,6 +1047,23 @@ static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
     w.alist = (int32_t *)p;
     p += align_up((size_t)ld * sizeof(int32_t), 256);
     w.acount = (int32_t *)p;
+    p += 256;
+    const size_t extra = ws_repack_bytes(code, ld);
+    w.repack = extra > 0 && ws_size >= ws_base_bytes(code, ld, max_it) + extra;
+    for (auto &r : w.rs) {
+        r = DecodeWs::RepackSet{nullptr, nullptr, nullptr, nullptr, nullptr};
+        if (!w.repack) continue;
+        r.c2v = (double *)p;
+        p += align_up((size_t)code->E * ld * sizeof(double), 256);
+        r.post = (double *)p;
+        p += align_up((size_t)code->V * ld * sizeof(double), 256);
+        r.lappr = (double *)p;
+        p += align_up((size_t)code->V * ld * sizeof(double), 256);
+        r.synd = (uint8_t *)p;
+        p += align_up((size_t)code->C * ld, 256);
+        r.fid = (int32_t *)p;
+        p += align_up((size_t)ld * sizeof(int32_t), 256);
+    }
     return w;
 }
 
@@ -970,9 +1071,17 @@ static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base) {
 struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3}, math{kStrict}, eps_max{40},
         lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024}, var_pace{28},
-        check_tail{4}, fused_iter{1}, iter_streams{2}, var_boost{4}, resident{1};
+        check_tail{4}, fused_iter{1}, iter_streams{2}, var_boost{4}, resident{1}, repack{1};
 };
 static Tuning g_tune;
+
+// knob repack (default 1): the workspace carries the two column sets of the repacked ranges
+// when the two-stream schedule can run (ld % 512 == 0) and they take at most 96 GiB
+static size_t ws_repack_bytes(const qr_code *code, int ld) {
+    if (!g_tune.repack.load() || ld % 512) return 0;
+    const size_t b = 2 * repack_set_bytes(code, ld);
+    return b <= ((size_t)96 << 30) ? b : 0;
+}
 
 // Frame tile ft (a divisor of ncols, <= ft_req) and nodes per thread.  Small problems (few
 // nodes x few frame tiles, e.g. the reg-(3,6) N=1008 code of configs[1]) get fewer nodes per
@@ -1008,6 +1117,8 @@ struct Plan {
     int lds_pad = 0;  // dynamic LDS reserved by each check workgroup (caps their CU residency)
     bool compact = false;  // sweeps of the main loop read the active-frame lists
     int var_pace = 0;      // variable sweeps: workgroups per 128 frames (0 = one per tile)
+    const int32_t *fid = nullptr;  // frame id of each column (a repacked range), or null
+    int32_t *hcount = nullptr;     // host-mapped copy of the status launches' counts, or null
 
     const int32_t *count_of(int f0) const { return w.acount + (f0 == 0 ? 0 : 1); }
 
@@ -1212,7 +1323,7 @@ static int launch_status(const Plan &P, int f0, int f1, int t, int final_call, i
     f1 = std::min(f1, P.B);
     if (f1 <= f0) return QR_OK;
     k_status<<<(f1 - f0 + 255) / 256, 256, 0, P.s>>>(f0, f1, t, final_call, final_iters, unsat_t, P.w.active,
-                                                     P.success, P.iters);
+                                                     P.success, P.iters, P.fid);
     QR_LAUNCH_CHECK();
     return QR_OK;
 }
@@ -1221,7 +1332,7 @@ static int launch_status(const Plan &P, int f0, int f1, int t, int final_call, i
 static int launch_compact(const Plan &P, int f0, int f1) {
     if (!P.compact) return QR_OK;
     k_compact<false><<<1, 1024, 0, P.s>>>(f0, f1, P.w.active, P.w.alist, const_cast<int32_t *>(P.count_of(f0)), 0,
-                                          nullptr, nullptr, nullptr);
+                                          nullptr, nullptr, nullptr, nullptr, nullptr);
     QR_LAUNCH_CHECK();
     return QR_OK;
 }
@@ -1232,7 +1343,8 @@ static int launch_status_compact(const Plan &P, int f0, int f1, int t, const uin
     if (!P.compact) return launch_status(P, f0, f1, t, 0, 0, unsat_t);
     ProfScope ps("status", P.s);
     k_compact<true><<<1, 1024, 0, P.s>>>(f0, f1, P.w.active, P.w.alist, const_cast<int32_t *>(P.count_of(f0)), t,
-                                         unsat_t, P.success, P.iters);
+                                         unsat_t, P.success, P.iters, P.fid,
+                                         P.hcount ? P.hcount + (f0 == 0 ? 0 : 1) : nullptr);
     QR_LAUNCH_CHECK();
     return QR_OK;
 }
@@ -1329,19 +1441,132 @@ static int side_stream(const qr_code *code, hipStream_t *out) {
     return QR_OK;
 }
 
-static int run_split2(const Plan &P, int max_it) {
+// Host-mapped counts and the status event rings of the column repack (caller holds code->mu;
+// all or nothing).
+// A decode still finishing on another stream may write its counts while the next one starts:
+// every decode takes the next of kRepackSlots count pairs.
+constexpr int kRepackSlots = 32;
+static int repack_resources(const qr_code *code) {
+    if (!code->hc) {
+        void *hp = nullptr, *dp = nullptr;
+        hipError_t e = hipHostMalloc(&hp, 2 * kRepackSlots * sizeof(int32_t), hipHostMallocMapped);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(&dp, hp, 0);
+        if (e != hipSuccess) {
+            if (hp) (void)hipHostFree(hp);
+            return set_error(QR_EDEVICE, "decode: host-mapped counts: %s", hipGetErrorString(e));
+        }
+        code->hc = (int32_t *)hp;
+        code->hc_dev = (int32_t *)dp;
+    }
+    if (!code->evs[0][0]) {
+        hipEvent_t ev[8] = {};
+        hipError_t e = hipSuccess;
+        for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+        if (e != hipSuccess) {
+            for (auto x : ev)
+                if (x) (void)hipEventDestroy(x);
+            return set_error(QR_EDEVICE, "decode: repack events: %s", hipGetErrorString(e));
+        }
+        for (int i = 0; i < 8; ++i) code->evs[i / 4][i % 4] = ev[i];
+    }
+    return QR_OK;
+}
+
+// One frame range of the two-stream schedule: columns [f0, f0 + w) of the caller's arrays
+// (set -1; the posteriors are the output itself) or of repack set w.rs[set].
+struct RangeLayout {
+    int f0, w, set;
+};
+
+static Plan layout_plan(const Plan &Q, const RangeLayout &L) {
+    Plan R = Q;
+    if (L.set >= 0) {
+        const auto &r = Q.w.rs[L.set];
+        R.lappr = r.lappr;
+        R.synd = r.synd;
+        R.post = r.post;
+        R.w.c2v = r.c2v;
+        R.fid = r.fid;
+        // the pacing spreads a full half's variable sweep over a full half's check launch (its
+        // paced length does not depend on the range's width); a repacked range's check launch
+        // is short, and so must be its variable sweep
+        R.var_pace = 0;
+    }
+    return R;
+}
+
+static unsigned gather_rows_grid(int64_t rows) { return (unsigned)std::min<int64_t>(rows, 2048); }
+
+// Move range L's running frames to the front of the other repack set (after its status launch,
+// on P.s); w_new >= the device count when the copy runs (counts only fall).
+static int repack_range(const Plan &P, RangeLayout &L, int w_new) {
+    const qr_code *code = P.code;
+    const int ld = P.ld;
+    const int dst_set = L.set < 0 ? 0 : 1 - L.set;
+    const auto &dst = P.w.rs[dst_set];
+    const Plan S = layout_plan(P, L);  // the current arrays
+    const int32_t *count = P.count_of(L.f0);
+    ProfScope ps("repack", P.s);
+    if (L.set >= 0) {  // frames stopped in this set hand their posteriors to the output first
+        k_scatter_post<<<dim3((unsigned)(L.w + 255) / 256, gather_rows_grid(code->V)), 256, 0, P.s>>>(
+            code->V, L.f0, L.w, ld, S.fid, P.w.active, 0, S.post, P.post);
+        QR_LAUNCH_CHECK();
+    }
+    const dim3 gx((unsigned)(w_new + 255) / 256);
+    k_gather_cols64<<<dim3(gx.x, gather_rows_grid(code->E)), 256, 0, P.s>>>(code->E, L.f0, ld, P.w.alist, count,
+                                                                            S.w.c2v, dst.c2v);
+    QR_LAUNCH_CHECK();
+    k_gather_cols64<<<dim3(gx.x, gather_rows_grid(code->V)), 256, 0, P.s>>>(code->V, L.f0, ld, P.w.alist, count,
+                                                                            S.lappr, dst.lappr);
+    QR_LAUNCH_CHECK();
+    k_gather_cols8<<<dim3(gx.x, gather_rows_grid(code->C)), 256, 0, P.s>>>(code->C, L.f0, ld, P.w.alist, count,
+                                                                           S.synd, dst.synd);
+    QR_LAUNCH_CHECK();
+    k_repack_flags<<<gx, 256, 0, P.s>>>(L.f0, w_new, P.w.alist, count, S.fid, dst.fid, P.w.active);
+    QR_LAUNCH_CHECK();
+    L.set = dst_set;
+    L.w = w_new;
+    return QR_OK;
+}
+
+// *finalized: the final parity check, status and output were issued here (a range was repacked).
+static int run_split2(const Plan &P, int max_it, bool *finalized) {
     const qr_code *code = P.code;
     std::lock_guard<std::mutex> lk(code->mu);
+    *finalized = false;
     hipStream_t s2 = nullptr;
     if (int rc0 = side_stream(code, &s2)) return rc0;
     hipEvent_t fork = code->ev[0], cA = code->ev[1], cB = code->ev[2], vA = code->ev[3], vB = code->ev[4];
+    const int ld = P.ld, h = ld / 2;
+    // Column repack (knob repack; needs the workspace's repack sets and a stream that is not
+    // being captured, since the host reads the counts back): after a range's status launch, the
+    // host waits for that range's previous status launch (the GPU still has about an iteration
+    // of work queued), reads its count, and repacks the range when its running frames fill at
+    // most half of its columns.
+    bool rp = P.compact && P.w.repack && g_tune.repack.load();
+    if (rp) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(P.s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) rp = false;
+    }
+    if (rp) {
+        if (int rc0 = repack_resources(code)) return rc0;
+    }
+    Plan Pb = P;  // status launches (P.s)
+    int32_t *hc = nullptr;
+    if (rp) {
+        const int slot = 2 * (int)(code->hc_gen++ % kRepackSlots);
+        hc = code->hc + slot;
+        Pb.hcount = code->hc_dev + slot;
+        hc[0] = hc[1] = ld;
+    }
     Plan V = P;
     V.s = s2;
     V.var_pace = g_tune.var_pace.load();
     Plan C = P;
     C.lds_pad = std::max(0, g_tune.lds_pad_kb.load()) * 1024;
-    const int ld = P.ld, h = ld / 2;
-    const int A0 = 0, A1 = h, B0 = h, B1 = ld;
+    RangeLayout L[2] = {{0, h, -1}, {h, ld - h, -1}};
+    int nstat[2] = {0, 0};
+    bool any_repack = false;
     auto row = [&](int t) { return P.w.unsat + (size_t)t * ld; };
     // Knob side (default 1): the check sweeps of the small degree classes (DVB-S2: the one
     // degree-6 check) run on the variable stream right after the variable sweep they follow,
@@ -1355,47 +1580,89 @@ static int run_split2(const Plan &P, int max_it) {
     for (int k = 0; k < (int)code->classes.size(); ++k)
         if (k != big) side_edges += code->classes[k].n * code->classes[k].degree;
     const bool side = g_tune.side.load() && code->classes.size() > 1 && side_edges * 8 <= code->E;
-    auto checks_main = [&](const Plan &Q, int t, int f0, int f1) {  // check sweep t >= 2 on Q's stream
-        if (!side) return launch_checks<kNormal>(Q, P.post, row(t - 1), f0, f1);
+    auto checks_main = [&](int t, int k) {  // check sweep t >= 2 of range k on the check stream
+        const Plan Q = layout_plan(C, L[k]);
+        const int f0 = L[k].f0, f1 = L[k].f0 + L[k].w;
+        if (!side) return launch_checks<kNormal>(Q, Q.post, row(t - 1), f0, f1);
         const DegreeClass &cls = code->classes[big];
-        return P.nt ? launch_check_class<kNormal, true>(Q, cls, P.post, row(t - 1), f0, f1)
-                    : launch_check_class<kNormal, false>(Q, cls, P.post, row(t - 1), f0, f1);
+        return P.nt ? launch_check_class<kNormal, true>(Q, cls, Q.post, row(t - 1), f0, f1)
+                    : launch_check_class<kNormal, false>(Q, cls, Q.post, row(t - 1), f0, f1);
     };
-    auto checks_side = [&](int t, int f0, int f1) {  // the other classes of check sweep t, on V.s
-        return side ? launch_checks<kNormal>(V, P.post, row(t - 1), f0, f1, big) : (int)QR_OK;
+    auto checks_side = [&](int t, int k) {  // the other classes of check sweep t, on V.s
+        if (!side) return (int)QR_OK;
+        const Plan Q = layout_plan(V, L[k]);
+        return launch_checks<kNormal>(Q, Q.post, row(t - 1), L[k].f0, L[k].f0 + L[k].w, big);
+    };
+    auto var_sweep = [&](int k) {
+        return launch_var<false>(layout_plan(V, L[k]), L[k].f0, L[k].f0 + L[k].w);
+    };
+    // status of sweep ts of range k (+ compaction), then the repack decision
+    auto status = [&](int k, int ts) -> int {
+        int rc0 = launch_status_compact(layout_plan(Pb, L[k]), L[k].f0, L[k].f0 + L[k].w, ts, row(ts));
+        if (rc0 || !rp) return rc0;
+        hipEvent_t *ring = code->evs[k];
+        QR_HIP(hipEventRecord(ring[nstat[k] % 4], P.s));
+        ++nstat[k];
+        if (nstat[k] < 2 || L[k].w <= 64) return QR_OK;
+        QR_HIP(hipEventSynchronize(ring[(nstat[k] - 2) % 4]));
+        const int cnt = *(volatile int32_t *)(hc + k);
+        if (cnt < 0 || cnt > L[k].w / 2) return QR_OK;
+        any_repack = true;
+        return repack_range(P, L[k], std::max(64, (cnt + 63) / 64 * 64));
     };
     int rc;
     QR_HIP(hipEventRecord(fork, P.s));
     QR_HIP(hipStreamWaitEvent(V.s, fork, 0));
-    if ((rc = launch_checks<kFirst>(C, P.post, row(0), A0, A1))) return rc;
+    if ((rc = launch_checks<kFirst>(C, P.post, row(0), 0, h))) return rc;
     QR_HIP(hipEventRecord(cA, P.s));
     for (int t = 1; t <= max_it; ++t) {
+        // every frame of both ranges has stopped (counts only fall; the host's copies lag): the
+        // remaining iterations would sweep nothing -- leave the loop with both ranges at a
+        // status boundary (B after S_B(t-1), A after S_A(t-1)); the final parity check and
+        // status below then find no running frame
+        if (rp && t >= 3 && *(volatile int32_t *)(hc + 0) == 0 && *(volatile int32_t *)(hc + 1) == 0) break;
         QR_HIP(hipStreamWaitEvent(V.s, cA, 0));
-        if ((rc = launch_var<false>(V, A0, A1))) return rc;
-        if (t < max_it && (rc = checks_side(t + 1, A0, A1))) return rc;
+        if ((rc = var_sweep(0))) return rc;
+        if (t < max_it && (rc = checks_side(t + 1, 0))) return rc;
         QR_HIP(hipEventRecord(vA, V.s));
         if (t == 1) {
-            if ((rc = launch_checks<kFirst>(C, P.post, row(0), B0, B1))) return rc;
+            if ((rc = launch_checks<kFirst>(C, P.post, row(0), h, ld))) return rc;
         } else {
             QR_HIP(hipStreamWaitEvent(P.s, vB, 0));
-            if ((rc = checks_main(C, t, B0, B1))) return rc;
-            if ((rc = launch_status_compact(P, B0, B1, t - 1, row(t - 1)))) return rc;
+            if ((rc = checks_main(t, 1))) return rc;
+            if ((rc = status(1, t - 1))) return rc;
         }
         QR_HIP(hipEventRecord(cB, P.s));
         if (t < max_it) {
             QR_HIP(hipStreamWaitEvent(P.s, vA, 0));
-            if ((rc = checks_main(C, t + 1, A0, A1))) return rc;
-            if ((rc = launch_status_compact(P, A0, A1, t, row(t)))) return rc;
+            if ((rc = checks_main(t + 1, 0))) return rc;
+            if ((rc = status(0, t))) return rc;
             QR_HIP(hipEventRecord(cA, P.s));
         }
         QR_HIP(hipStreamWaitEvent(V.s, cB, 0));
-        if ((rc = launch_var<false>(V, B0, B1))) return rc;
-        if (t < max_it && (rc = checks_side(t + 1, B0, B1))) return rc;
+        if ((rc = var_sweep(1))) return rc;
+        if (t < max_it && (rc = checks_side(t + 1, 1))) return rc;
         QR_HIP(hipEventRecord(vB, V.s));
     }
     // join: everything after (final parity check, status) follows both sweeps (vB follows cB)
     QR_HIP(hipStreamWaitEvent(P.s, vA, 0));
     QR_HIP(hipStreamWaitEvent(P.s, vB, 0));
+    if (!any_repack) return QR_OK;
+    // decoder.pyx:424-436 per range in its own columns: the parity of the last posteriors, the
+    // final status, then every frame of a repacked set hands its posteriors to the output
+    uint8_t *unsat_last = row(max_it);
+    for (int k = 0; k < 2; ++k) {
+        const Plan R = layout_plan(P, L[k]);
+        const int f0 = L[k].f0, f1 = L[k].f0 + L[k].w;
+        if ((rc = launch_checks<kParityOnly>(R, R.post, unsat_last, f0, f1))) return rc;
+        if ((rc = launch_status(R, f0, f1, max_it, 1, max_it, unsat_last))) return rc;
+        if (L[k].set >= 0) {
+            k_scatter_post<<<dim3((unsigned)(L[k].w + 255) / 256, gather_rows_grid(code->V)), 256, 0, P.s>>>(
+                code->V, f0, L[k].w, ld, R.fid, P.w.active, 1, R.post, P.post);
+            QR_LAUNCH_CHECK();
+        }
+    }
+    *finalized = true;
     return QR_OK;
 }
 
@@ -1525,12 +1792,13 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
         return set_error(QR_EVALUE, "decode: need 0 < B <= ld and ld %% 64 == 0 (B=%d, ld=%d)", B, ld);
     if (!lappr || !synd || !final_post || !success || !iters || !ws_ptr)
         return set_error(QR_EVALUE, "decode: null pointer argument");
-    if (ws_size < ws_bytes(code, ld, max_it))
-        return set_error(QR_EVALUE, "decode: workspace too small (%zu < %zu)", ws_size, ws_bytes(code, ld, max_it));
+    if (ws_size < ws_base_bytes(code, ld, max_it))
+        return set_error(QR_EVALUE, "decode: workspace too small (%zu < %zu)", ws_size,
+                         ws_base_bytes(code, ld, max_it));
     DeviceGuard dg(code->device);
     if (max_it > 0 && max_it <= kResMaxIter && resident_code(code))
         return run_resident(code, B, ld, lappr, synd, max_it, final_post, success, iters, s);
-    Plan P{code, B, ld, lappr, synd, final_post, success, iters, carve(code, ld, max_it, ws_ptr), g_tune.nt.load() != 0, s};
+    Plan P{code, B, ld, lappr, synd, final_post, success, iters, carve(code, ld, max_it, ws_ptr, ws_size), g_tune.nt.load() != 0, s};
     const int64_t rows = (int64_t)(max_it > 0 ? max_it : 0) + 2;  // no int overflow at INT_MAX
     int rc;
     QR_HIP(hipMemsetAsync(P.w.unsat, 0, (size_t)rows * ld, s));
@@ -1574,8 +1842,10 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     } else if ((rc = launch_compact(P, 0, ld))) {
         return rc;
     }
-    if ((rc = !split ? run_flat(P, max_it) : sp == 3 ? run_split2(P, max_it) : run_split(P, max_it)))
+    bool finalized = false;
+    if ((rc = !split ? run_flat(P, max_it) : sp == 3 ? run_split2(P, max_it, &finalized) : run_split(P, max_it)))
         return rc;
+    if (finalized) return QR_OK;
     // Check after the last sweep; then every frame still running stops with (0, max).
     const int tf = max_it > 0 ? max_it : 0;
     uint8_t *unsat_last = P.w.unsat + (size_t)tf * ld;
@@ -1668,6 +1938,10 @@ static int free_code(qr_code *c) {
     (void)hipFree(c->d_gtab);
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto &r : c->evs)
+        for (auto &e : r)
+            if (e) (void)hipEventDestroy(e);
+    if (c->hc) (void)hipHostFree(c->hc);
     if (c->s2) (void)hipStreamDestroy(c->s2);
     delete c;
     return QR_OK;
@@ -1784,7 +2058,7 @@ static std::atomic<int> *tune_knob(const char *name) {
         {"split_min_blocks", &g_tune.split_min_blocks},
         {"var_pace", &g_tune.var_pace},     {"check_tail", &g_tune.check_tail}, {"var_boost", &g_tune.var_boost},
         {"fused_iter", &g_tune.fused_iter}, {"iter_streams", &g_tune.iter_streams},
-        {"resident", &g_tune.resident},
+        {"resident", &g_tune.resident},   {"repack", &g_tune.repack},
     };
     const std::string n = name ? name : "";
     for (const auto &k : knobs)

@@ -110,6 +110,11 @@ struct qr_code {
     mutable std::mutex mu;
     mutable hipStream_t s2 = nullptr;
     mutable hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    // column repack of the two-stream schedule: host-mapped copies of the two ranges' running-
+    // frame counts and a ring of events per range after its status launches (created on first use)
+    mutable int32_t *hc = nullptr, *hc_dev = nullptr;  // kRepackSlots pairs, one per decode in turn
+    mutable unsigned hc_gen = 0;
+    mutable hipEvent_t evs[2][4] = {};
 };
 
 struct qr_demap {

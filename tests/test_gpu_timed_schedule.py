@@ -119,3 +119,38 @@ def test_reference_frames_in_timed_batch(gpu, fname, key, bps, snr, B):
             assert_bit_exact(f, g[f"{key}_final"])
         else:
             assert_bit_exact(f[g[f"{key}_sample_idx"]], g[f"{key}_sample_final"])
+
+
+@pytest.mark.parametrize("bps,snr,B", [(2, 4.0, 1024), (4, 14.5, 1024), (2, 3.8, 2048)])
+def test_column_repack_vs_oracle(gpu, bps, snr, B):
+    """Converging batches under the column repack (knob repack, default on: a range whose
+    running frames fill at most half its columns moves them to the front of a fresh column
+    set): every frame identical to the run without it, and the frames that ran longest --
+    the ones that went through the repacks -- bit-exact against the oracle."""
+    import torch
+    from qamr import _lib
+
+    _assert_timed_defaults()
+    vid, cid, dec, pipe, b = _pipeline(bps, snr, B, seed=300 + int(10 * snr))
+    lappr = pipe.demap(b)
+    saved = _lib.tune_get("repack")
+    outs = []
+    try:
+        for rp in (1, 0):
+            _lib.tune_set("repack", rp)
+            outs.append([x.clone() for x in pipe.decode(lappr, b)])
+            torch.cuda.synchronize()
+    finally:
+        _lib.tune_set("repack", saved)
+    (f1, s1, i1), (f0, s0, i0) = outs
+    assert torch.equal(s1, s0) and torch.equal(i1, i0)
+    assert torch.equal(f1[:, :B].view(torch.int64), f0[:, :B].view(torch.int64))
+    its = i1.cpu().numpy()
+    assert its.max() - its.min() >= 5  # frames stop over many iterations: ranges get repacked
+    cols = np.unique(np.r_[np.argsort(-its, kind="stable")[:8], _cols(B, 8)])
+    ct = torch.as_tensor(cols, device=lappr.device)
+    L = lappr[:, ct].T.contiguous().cpu().numpy()
+    Sy = b.synd[:, ct].T.contiguous().cpu().numpy()
+    s2, i2, fo = O.OracleCode(vid, cid).decode_batch(L, Sy, 50)
+    assert np.array_equal(s1[ct].cpu().numpy(), s2) and np.array_equal(i1[ct].cpu().numpy(), i2)
+    assert_bit_exact(f1[:, ct].T.contiguous().cpu().numpy(), fo)
