@@ -1520,7 +1520,7 @@ static unsigned gather_rows_grid(int64_t rows) { return (unsigned)std::min<int64
 
 // Move range L's running frames to the front of the other repack set (after its status launch,
 // on P.s); w_new >= the device count when the copy runs (counts only fall).
-static int repack_range(const Plan &P, RangeLayout &L, int w_new) {
+static int repack_range(const Plan &P, RangeLayout &L, int w_new) {  // on P.s
     const qr_code *code = P.code;
     const int ld = P.ld;
     const int dst_set = L.set < 0 ? 0 : 1 - L.set;
@@ -1615,10 +1615,18 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
         const Plan Q = layout_plan(V, L[k]);
         return launch_checks<kNormal>(Q, Q.post, row(t - 1), L[k].f0, L[k].f0 + L[k].w, big);
     };
+    int pending[2] = {0, 0};  // per range: the repacked width to apply before its next variable sweep
     auto var_sweep = [&](int k) {
+        if (pending[k]) {
+            if (int rc0 = repack_range(V, L[k], pending[k])) return rc0;
+            pending[k] = 0;
+        }
         return launch_var<false>(layout_plan(V, L[k]), L[k].f0, L[k].f0 + L[k].w);
     };
-    // status of sweep ts of range k (+ compaction), then the repack decision
+    // status of sweep ts of range k (+ compaction), then the repack decision; the repack itself
+    // is enqueued on the variable stream right before range k's next variable sweep (it waits
+    // for this status through the event that sweep waits on), so its copies run under the
+    // other range's check launch instead of on the check stream
     auto status = [&](int k, int ts) -> int {
         int rc0 = launch_status_compact(layout_plan(Pb, L[k]), L[k].f0, L[k].f0 + L[k].w, ts, row(ts));
         if (rc0 || !rp) return rc0;
@@ -1632,7 +1640,8 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
         const int w_new = std::max(64, (cnt + 63) / 64 * 64);
         if (w_new >= L[k].w) return QR_OK;
         any_repack = true;
-        return repack_range(P, L[k], w_new);
+        pending[k] = w_new;
+        return QR_OK;
     };
     int rc;
     QR_HIP(hipEventRecord(fork, P.s));
