@@ -1092,7 +1092,7 @@ struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3}, math{kStrict}, eps_max{40},
         lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024}, var_pace{28},
         check_tail{4}, fused_iter{1}, iter_streams{2}, var_boost{4}, resident{1}, repack{1},
-        repack_pct{65};
+        repack_pct{75};
 };
 static Tuning g_tune;
 
@@ -1563,8 +1563,10 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
     // being captured, since the host reads the counts back): after a range's status launch, the
     // host waits for that range's previous status launch (the GPU still has about an iteration
     // of work queued), reads its count, and repacks the range when its running frames fill at
-    // most repack_pct % of its columns (default 65; MI355X, 4-PAM 4.0 dB: 20.32-20.34 k frames/s
-    // at 65 %, 20.20-20.34 k at 50 %, 19.91-20.10 k at 35 %, 19.55 k without the repack).
+    // most repack_pct % of its columns (default 75; MI355X, 4-PAM 4.0 dB, copies on the variable
+    // stream: 20.25-20.26 k frames/s at 75 %, 20.21-20.22 k at 85 %, 20.07-20.14 k at 65 %;
+    // copies on the check stream, another box: 20.32-20.34 k at 65 %, 20.20-20.34 k at 50 %,
+    // 19.91-20.10 k at 35 %, 19.55 k without the repack).
     bool rp = P.compact && P.w.repack && g_tune.repack.load();
     if (rp) {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
