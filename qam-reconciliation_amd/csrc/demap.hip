@@ -126,6 +126,8 @@ __device__ __forceinline__ double g_inv_search_wave(const DemapTables &t, const 
 // in i order (noisemapper.pyx:521-530: per bit the reference's sequence of additions).  No
 // workgroup barrier: a wave's search lengths never hold up another wave.  The exact F_Y of the
 // closed-form root search is evaluated by the whole wave as in g_inv_search_wave.
+// 127 VGPRs, 4 waves/SIMD.  Forced to 5 / 6 waves (96 / 80 VGPRs, 108 / 160 B spilled per lane):
+// 16-PAM 44.2-44.3 / 44.6-44.7 ms vs 44.0-44.1, 4-PAM 16.9 / 19.1 ms vs 13.7 (MI355X, B = 4096).
 template <int BPS>
 __global__ void __launch_bounds__(256) k_demap_wave(const DemapTables *__restrict__ tab,
                                                     const MathTables *__restrict__ gmt, int B, int ld, int64_t S,

@@ -37,7 +37,7 @@ def _assert_timed_defaults():
         assert int(_lib.tune_get(k)) == v, f"bench default {k}={v} changed: update this test"
 
 
-def _pipeline(bps, snr, B, seed):
+def _pipeline(bps, snr, B, seed, max_iterations=50):
     import torch
     import qamr
     from qamr import codes
@@ -45,8 +45,8 @@ def _pipeline(bps, snr, B, seed):
 
     vid, cid = codes.dvbs2_like_half()
     dec = qamr.Decoder(vid, cid)
-    pipe = SofteningPipeline(dec, bps=bps, snr_db=snr, batch=B, max_iterations=50)
-    assert pipe.ld == B and B % 512 == 0  # run_split2 territory
+    pipe = SofteningPipeline(dec, bps=bps, snr_db=snr, batch=B, max_iterations=max_iterations)
+    assert pipe.ld % 512 == 0 and B > pipe.ld - 256  # run_split2 territory
     b = pipe.generate(torch.Generator(device="cuda").manual_seed(seed))
     return vid, cid, dec, pipe, b
 
@@ -121,8 +121,9 @@ def test_reference_frames_in_timed_batch(gpu, fname, key, bps, snr, B):
             assert_bit_exact(f[g[f"{key}_sample_idx"]], g[f"{key}_sample_final"])
 
 
-@pytest.mark.parametrize("bps,snr,B", [(2, 4.0, 1024), (4, 14.5, 1024), (2, 3.8, 2048)])
-def test_column_repack_vs_oracle(gpu, bps, snr, B):
+@pytest.mark.parametrize("bps,snr,B,mi", [(2, 4.0, 1024, 50), (4, 14.5, 1024, 50), (2, 3.8, 2048, 50),
+                                          (2, 4.0, 1000, 50), (2, 4.0, 1024, 22)])
+def test_column_repack_vs_oracle(gpu, bps, snr, B, mi):
     """Converging batches under the column repack (knob repack, default on: a range whose
     running frames fill at most half its columns moves them to the front of a fresh column
     set): every frame identical to the run without it, and the frames that ran longest --
@@ -131,7 +132,7 @@ def test_column_repack_vs_oracle(gpu, bps, snr, B):
     from qamr import _lib
 
     _assert_timed_defaults()
-    vid, cid, dec, pipe, b = _pipeline(bps, snr, B, seed=300 + int(10 * snr))
+    vid, cid, dec, pipe, b = _pipeline(bps, snr, B, seed=300 + int(10 * snr), max_iterations=mi)
     lappr = pipe.demap(b)
     saved = _lib.tune_get("repack")
     outs = []
@@ -146,11 +147,11 @@ def test_column_repack_vs_oracle(gpu, bps, snr, B):
     assert torch.equal(s1, s0) and torch.equal(i1, i0)
     assert torch.equal(f1[:, :B].view(torch.int64), f0[:, :B].view(torch.int64))
     its = i1.cpu().numpy()
-    assert its.max() - its.min() >= 5  # frames stop over many iterations: ranges get repacked
+    assert its.max() - its.min() >= 4  # frames stop over many iterations: ranges get repacked
     cols = np.unique(np.r_[np.argsort(-its, kind="stable")[:8], _cols(B, 8)])
     ct = torch.as_tensor(cols, device=lappr.device)
     L = lappr[:, ct].T.contiguous().cpu().numpy()
     Sy = b.synd[:, ct].T.contiguous().cpu().numpy()
-    s2, i2, fo = O.OracleCode(vid, cid).decode_batch(L, Sy, 50)
+    s2, i2, fo = O.OracleCode(vid, cid).decode_batch(L, Sy, mi)
     assert np.array_equal(s1[ct].cpu().numpy(), s2) and np.array_equal(i1[ct].cpu().numpy(), i2)
     assert_bit_exact(f1[:, ct].T.contiguous().cpu().numpy(), fo)
