@@ -21,7 +21,12 @@
 //                                    syndrome stop with (1, t-1)
 //   k_var                            post(t) = lappr + sum c2v (ascending edge)
 // plus an initial parity check of the input (decoder.pyx:400-405) and a final
-// parity check after the last sweep.
+// parity check after the last sweep.  Schedules (decode_batch_device): the two
+// frame halves pipelined on two streams (run_split2, the DVB-S2 default; the
+// running frames of a converging half are listed (k_compact) and, once they are
+// few, moved to contiguous columns (column repack)); all frames in lock-step
+// (run_flat); small codes with one launch per iteration (run_iter) or one launch
+// per decode with a workgroup per frame and its messages in LDS (k_resident).
 #include <atomic>
 
 #include "fastmath.hpp"
