@@ -28,6 +28,7 @@
 // (run_flat); small codes with one launch per iteration (run_iter) or one launch
 // per decode with a workgroup per frame and its messages in LDS (k_resident).
 #include <atomic>
+#include <functional>
 
 #include "fastmath.hpp"
 #include "glibc_math.hpp"
@@ -1097,7 +1098,7 @@ struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3}, math{kStrict}, eps_max{40},
         lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024}, var_pace{28},
         check_tail{4}, fused_iter{1}, iter_streams{2}, var_boost{4}, resident{1}, repack{1},
-        repack_pct{75};
+        repack_pct{75}, repack_lag0{1};
 };
 static Tuning g_tune;
 
@@ -1623,7 +1624,9 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
         return launch_checks<kNormal>(Q, Q.post, row(t - 1), L[k].f0, L[k].f0 + L[k].w, big);
     };
     int pending[2] = {0, 0};  // per range: the repacked width to apply before its next variable sweep
+    std::function<int(int)> decide_fn;
     auto var_sweep = [&](int k) {
+        if (int rc0 = decide_fn(k)) return rc0;
         if (pending[k]) {
             if (int rc0 = repack_range(V, L[k], pending[k])) return rc0;
             pending[k] = 0;
@@ -1637,12 +1640,25 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
     auto status = [&](int k, int ts) -> int {
         int rc0 = launch_status_compact(layout_plan(Pb, L[k]), L[k].f0, L[k].f0 + L[k].w, ts, row(ts));
         if (rc0 || !rp) return rc0;
-        hipEvent_t *ring = code->evs[k];
-        QR_HIP(hipEventRecord(ring[nstat[k] % 4], P.s));
+        QR_HIP(hipEventRecord(code->evs[k][nstat[k] % 4], P.s));
         ++nstat[k];
-        if (nstat[k] < 2 || L[k].w <= 64) return QR_OK;
-        QR_HIP(hipEventSynchronize(ring[(nstat[k] - 2) % 4]));
+        return QR_OK;
+    };
+    // The repack decision for range k, made right before its variable sweep is enqueued (the
+    // repack runs there).  Until the range's count first falls, the host reads the count of the
+    // status launch before the latest one (the GPU is an iteration ahead of that point: no
+    // bubble); from then on (knob repack_lag0, default 1) the latest one -- the variable stream
+    // waits for that status anyway, and the check stream still has the other launches queued.
+    int last_cnt[2] = {-1, -1};
+    bool conv[2] = {false, false};
+    auto decide = [&](int k) -> int {
+        if (!rp || nstat[k] < 1 || L[k].w <= 64) return QR_OK;
+        const bool lag0 = conv[k] && g_tune.repack_lag0.load();
+        if (!lag0 && nstat[k] < 2) return QR_OK;
+        QR_HIP(hipEventSynchronize(code->evs[k][(nstat[k] - (lag0 ? 1 : 2)) % 4]));
         const int cnt = *(volatile int32_t *)(hc + k);
+        if (last_cnt[k] >= 0 && cnt < last_cnt[k]) conv[k] = true;
+        last_cnt[k] = cnt;
         if (cnt < 0 || (int64_t)cnt * 100 > (int64_t)L[k].w * std::clamp(g_tune.repack_pct.load(), 1, 90)) return QR_OK;
         const int w_new = std::max(64, (cnt + 63) / 64 * 64);
         if (w_new >= L[k].w) return QR_OK;
@@ -1650,6 +1666,7 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
         pending[k] = w_new;
         return QR_OK;
     };
+    decide_fn = decide;
     int rc;
     QR_HIP(hipEventRecord(fork, P.s));
     QR_HIP(hipStreamWaitEvent(V.s, fork, 0));
@@ -2099,7 +2116,7 @@ static std::atomic<int> *tune_knob(const char *name) {
         {"var_pace", &g_tune.var_pace},     {"check_tail", &g_tune.check_tail}, {"var_boost", &g_tune.var_boost},
         {"fused_iter", &g_tune.fused_iter}, {"iter_streams", &g_tune.iter_streams},
         {"resident", &g_tune.resident},   {"repack", &g_tune.repack},
-        {"repack_pct", &g_tune.repack_pct},
+        {"repack_pct", &g_tune.repack_pct}, {"repack_lag0", &g_tune.repack_lag0},
     };
     const std::string n = name ? name : "";
     for (const auto &k : knobs)
