@@ -487,6 +487,73 @@ __global__ void __launch_bounds__(256) k_var(VarArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Narrow sweeps of a repacked range of at most 64 columns (the last running frames of a
+// converging batch).  The frame-parallel sweeps give every check a 64-lane wave of frames, so a
+// range with a handful of running frames still pays a whole wave per check; here a wave is 16
+// frames x 4 checks (lane = (check, frame), kNarrowFrames frames per group, one group per
+// blockIdx.y): the 16 frames of a group are consecutive columns, so each message row access is
+// one 128-byte line, and a group with no listed frame leaves at once.  The CSR is read per lane.
+// Each message is the same operation on the same operands as in check_block / var_block.
+constexpr int kNarrowFrames = 16;
+constexpr int kNarrowNodes = 256 / kNarrowFrames;  // checks (variables) per workgroup
+
+template <int D, bool FIN>
+__device__ __forceinline__ void check_narrow_block(const CheckArgs &a, const GlibcTablesBP &tab, double *hb) {
+    bool live;
+    const int p = (int)blockIdx.y * kNarrowFrames + (int)(threadIdx.x % kNarrowFrames);
+    const int f = lane_frame(a.alist, a.acount, a.f_off, p, live);
+    const bool act = live && a.active[f] != 0;
+    if (!wave_any(act)) return;  // wave-uniform: the packed update needs whole waves
+    const int64_t ci = (int64_t)blockIdx.x * kNarrowNodes + (int64_t)(threadIdx.x / kNarrowFrames);
+    const bool valid = ci < a.n_checks;
+    const int cc = a.checks[valid ? ci : a.n_checks - 1];
+    const int base = a.chk_ptr[cc];
+    const size_t ld = a.ld;
+    const uint8_t sb = a.synd[(size_t)cc * ld + f];
+    uint32_t par = sb;
+    double m[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        const double pv = a.post[(size_t)a.chk_var[base + i] * ld + f];
+        par ^= (pv < 0.0) ? 1u : 0u;                                  // decoder.pyx:243-246
+        m[i] = pv - a.c2v[(size_t)a.chk_edge[base + i] * ld + f];      // :296-297
+    }
+    double out[D];
+    check_strict_packed<D, FIN ? kClampFinite : kClampFull>(m, out, hb + (threadIdx.x >> 6) * kPackWaveDoubles, tab,
+                                                            Arith<kStrict>::regs());
+    const double s = sb ? -1.0 : 1.0;
+    if (valid && act) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) a.c2v[(size_t)a.chk_edge[base + i] * ld + f] = s * out[i];
+        if (par == 1u) a.unsat[f] = 1;  // benign race: every writer stores 1
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) k_check_narrow(CheckArgs a) {
+    __shared__ GlibcTablesBP tab;
+    __shared__ double hb[4 * kPackWaveDoubles];
+    if (!frames_block_live(a.acount, blockIdx.y * kNarrowFrames, 0)) return;  // block-uniform
+    stage_glibc_tables(&tab, a.gglibc);
+    if (a.finite && sld(a.finite)) check_narrow_block<D, true>(a, tab, hb);
+    else check_narrow_block<D, false>(a, tab, hb);
+}
+
+__global__ void __launch_bounds__(256) k_var_narrow(VarArgs a) {
+    if (!frames_block_live(a.acount, blockIdx.y * kNarrowFrames, 0)) return;  // block-uniform
+    bool live;
+    const int p = (int)blockIdx.y * kNarrowFrames + (int)(threadIdx.x % kNarrowFrames);
+    const int f = lane_frame(a.alist, a.acount, a.f_off, p, live);
+    const int64_t v = (int64_t)blockIdx.x * kNarrowNodes + (int64_t)(threadIdx.x / kNarrowFrames);
+    if (!live || v >= a.V || !a.active[f]) return;
+    const size_t ld = a.ld;
+    double pv = a.lappr[(size_t)v * ld + f];
+    const int b = a.var_ptr[v], e = a.var_ptr[v + 1];
+    for (int k = b; k < e; ++k) pv += a.c2v[(size_t)a.var_edge[k] * ld + f];  // decoder.pyx:292-293
+    a.post[(size_t)v * ld + f] = pv;
+}
+
+// ---------------------------------------------------------------------------------------
 // Small codes (configs[1], reg-(3,6) N=1008): ONE launch per iteration.  A sweep of such a
 // code is a few microseconds of chip work, so the three launches of the flat schedule
 // (check, status, variable) are dominated by dispatch and drain.  Here the check sweep
@@ -1098,7 +1165,7 @@ struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3}, math{kStrict}, eps_max{40},
         lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024}, var_pace{28},
         check_tail{4}, fused_iter{1}, iter_streams{2}, var_boost{4}, resident{1}, repack{1},
-        repack_pct{75}, repack_lag0{1};
+        repack_pct{75}, repack_lag0{1}, narrow{1};
 };
 static Tuning g_tune;
 
@@ -1145,6 +1212,7 @@ struct Plan {
     bool compact = false;  // sweeps of the main loop read the active-frame lists
     int var_pace = 0;      // variable sweeps: workgroups per 128 frames (0 = one per tile)
     const int32_t *fid = nullptr;  // frame id of each column (a repacked range), or null
+    bool narrow = false;           // a repacked range: sweeps of <= 64 columns take the narrow kernels
     int32_t *hcount = nullptr;     // host-mapped copy of the status launches' counts, or null
 
     const int32_t *count_of(int f0) const { return w.acount + (f0 == 0 ? 0 : 1); }
@@ -1242,6 +1310,24 @@ static int launch_check_class(const Plan &P, const DegreeClass &cls, const doubl
                                       std::to_string(cls.degree)
                                 : std::string(),
                  P.s);
+    // knob narrow (default 1): a repacked range of <= 64 columns, strict packed degrees
+    if (MODE == kNormal && P.narrow && P.compact && ar == kStrict && cls.degree >= 2 && cls.degree <= kPackMaxDeg &&
+        f1 - f0 <= 64) {
+        const dim3 gn((unsigned)((cls.n + kNarrowNodes - 1) / kNarrowNodes),
+                      (unsigned)((f1 - f0 + kNarrowFrames - 1) / kNarrowFrames));
+#define QR_NARROW(DD)                                         \
+    case DD:                                                  \
+        k_check_narrow<DD><<<gn, 256, 0, P.s>>>(a);           \
+        break;
+        switch (cls.degree) {
+            QR_NARROW(2) QR_NARROW(3) QR_NARROW(4) QR_NARROW(5) QR_NARROW(6) QR_NARROW(7) QR_NARROW(8) QR_NARROW(9)
+            QR_NARROW(10)
+            default: break;
+        }
+#undef QR_NARROW
+        QR_LAUNCH_CHECK();
+        return QR_OK;
+    }
 #define QR_CASE(DD)                                                                                   \
     case DD:                                                                                          \
         if (ar == kStrict) k_check<DD, MODE, NT, kStrict><<<grid, 256, P.lds_pad, P.s>>>(a);          \
@@ -1284,6 +1370,13 @@ static int launch_var(const Plan &P, int f0, int f1, int32_t *finite = nullptr, 
     if (P.compact && !INIT) {
         a.alist = P.w.alist;
         a.acount = P.count_of(f0);
+    }
+    if (!INIT && P.narrow && P.compact && f1 - f0 <= 64) {  // a repacked range (knob narrow)
+        const dim3 gn((unsigned)((P.code->V + kNarrowNodes - 1) / kNarrowNodes),
+                      (unsigned)((f1 - f0 + kNarrowFrames - 1) / kNarrowFrames));
+        k_var_narrow<<<gn, 256, 0, P.s>>>(a);
+        QR_LAUNCH_CHECK();
+        return QR_OK;
     }
     dim3 grid(a.nbx, a.nby);
     // Paced sweep (the two-stream schedule's variable sweeps, Plan::var_pace): at most var_pace
@@ -1514,6 +1607,7 @@ static Plan layout_plan(const Plan &Q, const RangeLayout &L) {
         R.post = r.post;
         R.w.c2v = r.c2v;
         R.fid = r.fid;
+        R.narrow = g_tune.narrow.load() != 0;
         // the pacing spreads a full half's variable sweep over a full half's check launch (its
         // paced length does not depend on the range's width); a repacked range's check launch
         // is short, and so must be its variable sweep
@@ -2116,7 +2210,7 @@ static std::atomic<int> *tune_knob(const char *name) {
         {"var_pace", &g_tune.var_pace},     {"check_tail", &g_tune.check_tail}, {"var_boost", &g_tune.var_boost},
         {"fused_iter", &g_tune.fused_iter}, {"iter_streams", &g_tune.iter_streams},
         {"resident", &g_tune.resident},   {"repack", &g_tune.repack},
-        {"repack_pct", &g_tune.repack_pct}, {"repack_lag0", &g_tune.repack_lag0},
+        {"repack_pct", &g_tune.repack_pct}, {"repack_lag0", &g_tune.repack_lag0}, {"narrow", &g_tune.narrow},
     };
     const std::string n = name ? name : "";
     for (const auto &k : knobs)

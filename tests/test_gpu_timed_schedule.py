@@ -134,18 +134,23 @@ def test_column_repack_vs_oracle(gpu, bps, snr, B, mi):
     _assert_timed_defaults()
     vid, cid, dec, pipe, b = _pipeline(bps, snr, B, seed=300 + int(10 * snr), max_iterations=mi)
     lappr = pipe.demap(b)
-    saved = _lib.tune_get("repack")
+    saved = {k: _lib.tune_get(k) for k in ("repack", "narrow")}
     outs = []
     try:
-        for rp in (1, 0):
+        # repacked ranges of <= 64 columns on the narrow (lane = (check, frame)) sweeps / on the
+        # frame-parallel ones; then no repack at all
+        for rp, nw in ((1, 1), (1, 0), (0, 1)):
             _lib.tune_set("repack", rp)
+            _lib.tune_set("narrow", nw)
             outs.append([x.clone() for x in pipe.decode(lappr, b)])
             torch.cuda.synchronize()
     finally:
-        _lib.tune_set("repack", saved)
-    (f1, s1, i1), (f0, s0, i0) = outs
-    assert torch.equal(s1, s0) and torch.equal(i1, i0)
-    assert torch.equal(f1[:, :B].view(torch.int64), f0[:, :B].view(torch.int64))
+        for k, v in saved.items():
+            _lib.tune_set(k, v)
+    f1, s1, i1 = outs[0]
+    for f0, s0, i0 in outs[1:]:
+        assert torch.equal(s1, s0) and torch.equal(i1, i0)
+        assert torch.equal(f1[:, :B].view(torch.int64), f0[:, :B].view(torch.int64))
     its = i1.cpu().numpy()
     assert its.max() - its.min() >= 4  # frames stop over many iterations: ranges get repacked
     cols = np.unique(np.r_[np.argsort(-its, kind="stable")[:8], _cols(B, 8)])
