@@ -1747,11 +1747,12 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
     bool conv[2] = {false, false};
     auto decide = [&](int k) -> int {
         if (!rp || nstat[k] < 1 || L[k].w <= 64) return QR_OK;
-        const bool lag0 = conv[k] && g_tune.repack_lag0.load();
+        // the two ranges converge together: a fall seen in either switches both
+        const bool lag0 = (conv[0] || conv[1]) && g_tune.repack_lag0.load();
         if (!lag0 && nstat[k] < 2) return QR_OK;
         QR_HIP(hipEventSynchronize(code->evs[k][(nstat[k] - (lag0 ? 1 : 2)) % 4]));
         const int cnt = *(volatile int32_t *)(hc + k);
-        if (last_cnt[k] >= 0 && cnt < last_cnt[k]) conv[k] = true;
+        if (last_cnt[k] >= 0 && cnt < last_cnt[k]) conv[k] = true;  // (a lag-0 read never precedes a lag-1 one)
         last_cnt[k] = cnt;
         if (cnt < 0 || (int64_t)cnt * 100 > (int64_t)L[k].w * std::clamp(g_tune.repack_pct.load(), 1, 90)) return QR_OK;
         const int w_new = std::max(64, (cnt + 63) / 64 * 64);
