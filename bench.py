@@ -58,7 +58,6 @@ GUIDE_COPY_GBS = 6290.0  # float4 streaming copy measured on MI355X (MI355X_MICR
 # fp64 VALU: 78.6 TFLOP/s spec = 1024 SIMDs x 2.4 GHz x 16 fp64 FMA lanes: a wave64 fp64
 # instruction occupies its SIMD 4 cycles, 32-bit VALU 2 cycles (MI355X_MICROARCH.md).
 SIMDS, CLOCK_HZ = 1024, 2.4e9
-MATH = {"strict": 0, "fast": 1, "eps": 2}
 # launches timed with hipEvents inside the timed region: the roofline's dominant kernel
 # (k_check<7> under the default schedule, k_fused<7> under split = 2) and the fused demap
 PRICED = ("check_d7", "fused_d7", "demap")
@@ -88,8 +87,6 @@ def parse(argv=None):
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (0 = skip)")
     p.add_argument("--no-roofline", action="store_true", help="skip per-kernel event timing")
-    p.add_argument("--math", default="strict", choices=list(MATH), help="decoder arithmetic (strict = bit-exact)")
-    p.add_argument("--no-alt", action="store_true", help="skip the alt_math throughput of the other arithmetics")
     p.add_argument("--no-secondary", action="store_true", help="skip the secondary configs")
     p.add_argument("--graph", type=int, default=0, choices=[0, 1],
                    help="1: replay each step as a captured HIP graph (kernel timings then come from the "
@@ -351,8 +348,6 @@ def roofline(args, w, kstats, dev, world=1):
     """The dominant kernel's algorithmic bytes per launch / its average launch time."""
     import qamr
 
-    math_mode = int(qamr._lib.tune_get("math"))
-    ar = {0: "kStrict", 1: "kFast", 2: "kEps"}.get(math_mode, "?")
     B, ld = w.B, w.batch.ld
     if "fused_d7" in kstats:
         # split = 2: one launch = check sweep of one frame half + variable sweep of the other
@@ -362,7 +357,7 @@ def roofline(args, w, kstats, dev, world=1):
         bc0, _ = check_class_bytes(w.vid, w.cid, 7, fr_c)
         bc1, _ = check_class_bytes(w.vid, w.cid, 7, max(B - fr_c, 0))
         bytes_launch = (bc0 + bc1) / 2 + (var_sweep_bytes(w.V, w.E, fr_c) + var_sweep_bytes(w.V, w.E, fr_v)) / 2
-        kname = f"k_fused<7,Normal,{ar}> (check sweep of one frame half + variable sweep of the other)"
+        kname = f"k_fused<7,Normal> (check sweep of one frame half + variable sweep of the other)"
         kkey = "fused_d7"
     elif "check_d7" in kstats:
         if int(qamr._lib.tune_get("split")) >= 3 and ld % 512 == 0:
@@ -373,11 +368,11 @@ def roofline(args, w, kstats, dev, world=1):
             bc0, _ = check_class_bytes(w.vid, w.cid, 7, fr_c)
             bc1, _ = check_class_bytes(w.vid, w.cid, 7, max(B - fr_c, 0))
             bytes_launch = (bc0 + bc1) / 2
-            kname = (f"k_check<7,Normal,{ar}> (check sweep of one frame half; the variable sweep of the "
+            kname = ("k_check<7,Normal> (check sweep of one frame half; the variable sweep of the "
                      f"other half runs concurrently on a second stream)")
         else:
             bytes_launch, _ = check_class_bytes(w.vid, w.cid, 7, B)
-            kname = f"k_check<7,Normal,{ar}> (degree-7 check-node sweep)"
+            kname = "k_check<7,Normal> (degree-7 check-node sweep)"
         kkey = "check_d7"
     else:
         return None
@@ -389,7 +384,7 @@ def roofline(args, w, kstats, dev, world=1):
         try:
             t = json.load(open(pmc))
             if t.get("workload") == args.workload and int(t.get("batch", -1)) == B \
-                    and t.get("kernel_key") == kkey and t.get("math") == math_mode:
+                    and t.get("kernel_key") == kkey and t.get("math", 0) == 0:
                 traffic = t.get("hbm_bytes_per_launch")
                 if t.get("valu_insts_per_launch"):
                     n_all, n64 = t["valu_insts_per_launch"], t.get("valu_f64_insts_per_launch", 0)
@@ -510,29 +505,6 @@ def cpu_baseline(args, w, budget_s):
     return out
 
 
-def alt_math(args, w):
-    """The other arithmetics on the same resident batch (not the measured value)."""
-    import qamr
-
-    alt = {}
-    for name, code in MATH.items():
-        if name == args.math:
-            continue
-        qamr._lib.tune_set("math", code)
-        w.step_eager()  # (a captured graph would replay the measured arithmetic's kernels)
-        w.sync()
-        n_alt = 2
-        ta = time.perf_counter()
-        for _ in range(n_alt):
-            w.step_eager()
-        w.sync()
-        alt[name] = round(w.B * n_alt / (time.perf_counter() - ta), 1)
-    qamr._lib.tune_set("math", MATH[args.math])
-    w.step_eager()  # leave `final` as the measured arithmetic produced it
-    w.sync()
-    return alt
-
-
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else list(argv)
     args = parse(argv)
@@ -561,7 +533,6 @@ def main(argv=None):
         if qamr.device_count() <= 0:
             raise SystemExit("bench: no HIP device")
         torch.cuda.set_device(local)
-        qamr._lib.tune_set("math", MATH[args.math])
         w = Work(args.workload, args.snr, args.batch, args.max_iter, args.alpha, args.seed, rank, local)
 
     prof = not stub and not args.no_roofline
@@ -618,7 +589,6 @@ def main(argv=None):
         it_mean = w.mean_iterations()
         # whole-decode algorithmic bandwidth (SURVEY.md 8(d) B_frame at the iterations actually run)
         B_frame = 16 * w.V + w.C + it_mean * (24 * w.E + 24 * w.V + w.C)
-        alt = alt_math(args, w) if (world == 1 and not args.no_alt) else None
         cpu = None
         if rank == 0 and world == 1 and args.cpu_seconds > 0:
             cpu = cpu_baseline(args, w, args.cpu_seconds)
@@ -628,17 +598,12 @@ def main(argv=None):
                          "snr_db": w.snr, "bps": w.bps, "fused_demap": w.fused, "parallelism": f"dp{world}",
                          "hip_graph": graph,
                          "backend": dist.backend() or "none", "rank_devices": rank_devices,
-                         "arithmetic": args.math + (" (glibc exp/log restated: outputs bit-identical to the "
-                                                    "reference)" if args.math == "strict" else
-                                                    " (approximate, opt-in)")}
+                         "arithmetic": "strict (glibc exp/log restated: outputs bit-identical to the reference)"}
         if dev_pin is not None:
             out["config"]["rehearsal"] = f"all {world} ranks on GPU {dev_pin}"
         out.update({
             "roofline": roof,
             "cpu_baseline": cpu,
-            "alt_math": {"frames_per_s": alt, "note": "opt-in approximate arithmetics, same batch, 2 steps each; "
-                                                      "not bit-exact (1e-6 LAPPR bar met at configs[2] only)"}
-            if alt else None,
             "decode_alg_GBps": round(B_frame * total_frames / elapsed / 1e9, 1),
             "mean_iterations": it_mean,
             "ber_fer": {"ber": ber, "fer": fer, "avg_iters_success": avg_it, "frames_counted": int(counters[4])},

@@ -30,7 +30,6 @@
 #include <atomic>
 #include <functional>
 
-#include "fastmath.hpp"
 #include "glibc_math.hpp"
 #include "qamr_internal.hpp"
 #include "strict_pack.hpp"
@@ -40,34 +39,11 @@ namespace qr {
 
 enum CheckMode { kFirst = 0, kNormal = 1, kParityOnly = 2 };
 
-// Check-node arithmetic (knob "math"):
-//   kStrict -- the reference's box-plus bit for bit: glibc exp/log restated
-//              (glibc_math.hpp), so every message, posterior and output LAPPR is
-//              identical to the reference's;
-//   kFast   -- box-plus with the table h(t) of fastmath.hpp (<= ulp(1) per h);
-//   kEps    -- the exp-domain update of fastmath.hpp (lanes with inputs beyond
-//              eps_max take the kFast box-plus).
-enum MathMode { kStrict = 0, kFast = 1, kEps = 2 };
-
-// Tab: the tables staged in LDS; Regs: per-thread constants kept in VGPRs.
-template <int AR>
-struct Arith {  // kFast, kEps: MathTables (10 KiB) in LDS
-    using Tab = MathTables;
-    struct Regs {};
-    static __device__ __forceinline__ Regs regs() { return Regs{}; }
-    static __device__ __forceinline__ double bp(double a, double b, const Tab &T, const Regs &) {
-        return box_plus_fast(a, b, T);
-    }
-};
-template <>
-struct Arith<kStrict> {  // the box-plus part of GlibcTables (8 KiB) in LDS
-    using Tab = GlibcTablesBP;
-    using Regs = GlibcK;
-    static __device__ __forceinline__ Regs regs() { return GlibcK::pinned(); }
-    static __device__ __forceinline__ double bp(double a, double b, const Tab &T, const Regs &K) {
-        return box_plus_strict(a, b, T, K);
-    }
-};
+// Check-node arithmetic: the reference's box-plus bit for bit -- glibc exp/log restated
+// (glibc_math.hpp, the box-plus part of its tables, 8 KiB, staged in LDS per workgroup; a few
+// constants pinned in VGPRs, GlibcK) -- so every message, posterior and output LAPPR is
+// identical to the reference's.  (Rounds 1-4 also carried two approximate arithmetics; they
+// missed north_star's 1e-6 LAPPR bar at configs[3] and were removed.)
 
 // Edge-message access: NT = non-temporal (streamed once per sweep; keeps the
 // re-read posteriors resident in L2/MALL instead of the message stream).
@@ -144,9 +120,7 @@ struct CheckArgs {
     int ld, f_off;
     Geom g;
     unsigned nbx;  // blocks along the check axis
-    const MathTables *gtab;
     const GlibcTables *gglibc;
-    double eps_max;      // exp-domain inputs: |m| <= eps_max (<= kEpsMax)
     double *fb;          // runtime-degree kernel: F scratch of the class (row fb_base)
     int64_t fb_base;
     const int32_t *alist;   // active-frame list (frame ids at alist[f_off + p]) or null
@@ -200,11 +174,6 @@ __device__ __forceinline__ int lane_frame(const int32_t *alist, const int32_t *a
     return alist[f_off + (live ? p : cnt - 1)];
 }
 
-template <int AR>
-__device__ __forceinline__ void stage_tables(typename Arith<AR>::Tab *lds, const CheckArgs &a) {
-    if constexpr (AR == kStrict) stage_glibc_tables(lds, a.gglibc);
-    else stage_math_tables(lds, a.gtab);
-}
 
 // The inputs of one check update: gathered posteriors, own c2v messages, syndrome bit.
 // The gathered posteriors of check j+1 are issued before the arithmetic of check j on the
@@ -245,25 +214,22 @@ constexpr int kPackMaxDeg = 10;
 // keeps finite.  The check sweeps then run the packed update with the one-instruction clamp
 // (strict_pack.hpp kClampFinite) instead of the NaN-preserving two-instruction one.
 // LDS of the packed strict update: one buffer per wavefront of a block.
-template <int AR>
-struct PackLds {
-    static constexpr int doubles = AR == kStrict ? 4 * kPackWaveDoubles : 1;
-};
-template <int AR, int D>
-constexpr bool kPacked = AR == kStrict && D <= kPackMaxDeg;
+constexpr int kPackLdsDoubles = 4 * kPackWaveDoubles;
+template <int D>
+constexpr bool kPacked = D <= kPackMaxDeg;
 
-// decoder.pyx:322-369 for one check with the box-plus of Arith<AR>.
+// decoder.pyx:322-369 for one check (strict box-plus).
 // Packed strict update (D <= kPackMaxDeg): strict_pack.hpp.  Otherwise
 // F[i] = bp(F[i-1], m[i]); the backward values B[i] = bp(B[i+1], m[i]) are consumed as
 // they are produced (out_i = bp(F[i-1], B[i+1])): the same operands as
 // decoder.pyx:341-367, one live B instead of D.  Lane byte offset b8 = f * 8.
-template <int AR, int D, bool NT, bool FIN = false>
+template <int D, bool NT, bool FIN = false>
 __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m)[D], int base, uint8_t sb, uint32_t b8,
-                                            const typename Arith<AR>::Tab &tab, const typename Arith<AR>::Regs &K,
-                                            double *hb = nullptr, bool live = true) {
+                                            const GlibcTablesBP &tab, const GlibcK &K, double *hb = nullptr,
+                                            bool live = true) {
     const int ld = a.ld;
     const double s = sb ? -1.0 : 1.0;
-    if constexpr (kPacked<AR, D>) {
+    if constexpr (kPacked<D>) {
         double out[D];
         double *wb = hb + (threadIdx.x >> 6) * kPackWaveDoubles;
         check_strict_packed<D, FIN ? kClampFinite : kClampFull>(m, out, wb, tab, K);
@@ -275,14 +241,14 @@ __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m
     double F[D - 1];
     F[0] = m[0];
 #pragma unroll
-    for (int i = 1; i < D - 1; ++i) F[i] = Arith<AR>::bp(F[i - 1], m[i], tab, K);
+    for (int i = 1; i < D - 1; ++i) F[i] = box_plus_strict(F[i - 1], m[i], tab, K);
     if (live) st_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + D - 1), ld), b8, ld, s * F[D - 2]);
     double Bn = m[D - 1];
 #pragma unroll
     for (int i = D - 2; i > 0; --i) {
-        const double o = s * Arith<AR>::bp(F[i - 1], Bn, tab, K);
+        const double o = s * box_plus_strict(F[i - 1], Bn, tab, K);
         if (live) st_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), ld), b8, ld, o);
-        Bn = Arith<AR>::bp(Bn, m[i], tab, K);
+        Bn = box_plus_strict(Bn, m[i], tab, K);
     }
     if (live) st_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base), ld), b8, ld, s * Bn);
 }
@@ -291,13 +257,9 @@ __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m
 // decoder.pyx:322-369 (F/B recursion) with the parity test of decoder.pyx:235-257
 // fused on the posteriors it gathers anyway.  Unpacked paths are software-pipelined: the
 // posterior gathers of check j+1 are issued before the box-plus arithmetic of check j.
-// EPS: the update runs in the exp domain (fastmath.hpp::check_node_eps, ~2.4x fewer
-// VALU instructions) in every lane whose inputs are all in its domain, the exact path
-// in the others; a wave whose lanes agree runs one path only (the other is skipped
-// under an empty exec mask), and a frame's result never depends on its wave-mates.
-template <int D, int MODE, bool NT, int AR, bool FIN = false>
+template <int D, int MODE, bool NT, bool FIN = false>
 __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, unsigned by, int per,
-                                            const typename Arith<AR>::Tab &tab, double *hb) {
+                                            const GlibcTablesBP &tab, double *hb) {
     const int ft = 1 << a.g.lft;
     const int nsub = 256 >> a.g.lft;
     bool live;
@@ -313,8 +275,8 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
     int64_t ci = (int64_t)bx * per * nsub + sub;
     if (ci >= a.n_checks) return;
     uint32_t bad = 0;
-    const auto K = Arith<AR>::regs();
-    constexpr bool kPrefetch = !kPacked<AR, D>;
+    const auto K = GlibcK::pinned();
+    constexpr bool kPrefetch = !kPacked<D>;
     CheckIn<D, MODE, NT> nx;
     nx.load(a, ci, f);
     for (int j = 0; j < per; ++j) {
@@ -336,22 +298,7 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
         if (MODE != kFirst) bad |= (par == 1u) ? 1u : 0u;  // satisfied iff (parity ^ 1) != 0
         if (MODE != kParityOnly) {
             const uint32_t b8 = (uint32_t)f * 8u;
-            if constexpr (AR == kEps) {
-                bool in = true;
-#pragma unroll
-                for (int i = 0; i < D; ++i) in &= eps_ok(m[i], a.eps_max);
-                // per lane: a wave whose lanes all agree runs one path (execz skips the other)
-                if (in || !act) {  // stopped lanes never force the exact path
-                    const int base = cur.base;
-                    check_node_eps<D>(m, cur.sb, tab, [&](int i, double v) {
-                        if (live) st_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), a.ld), b8, a.ld, v);
-                    });
-                } else {
-                    check_exact<kFast, D, NT>(a, m, cur.base, cur.sb, b8, tab, Arith<kFast>::Regs{}, nullptr, live);
-                }
-            } else {
-                check_exact<AR, D, NT, FIN>(a, m, cur.base, cur.sb, b8, tab, K, hb, live);
-            }
+            check_exact<D, NT, FIN>(a, m, cur.base, cur.sb, b8, tab, K, hb, live);
         }
         if (!more) break;
         if (!kPrefetch) nx.load(a, cn, f);
@@ -429,10 +376,10 @@ struct ClkScope {
     }
 };
 #endif
-template <int D, int MODE, bool NT, int AR>
+template <int D, int MODE, bool NT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) k_check(CheckArgs a) {
-    __shared__ typename Arith<AR>::Tab tab;
-    __shared__ double hb[PackLds<AR>::doubles];
+    __shared__ GlibcTablesBP tab;
+    __shared__ double hb[kPackLdsDoubles];
     unsigned bx = blockIdx.x, by = blockIdx.y;
     int per = a.g.per;
     if (a.nmain) {  // short-tail 1-D grid (block-uniform)
@@ -447,16 +394,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
     }
     if (!frames_block_live(a.acount, by, a.g.lft)) return;  // block-uniform
 #if QR_EXPERIMENT_CLOCK
-    ClkScope clk(D == 7 && MODE == kNormal && AR == kStrict);
+    ClkScope clk(D == 7 && MODE == kNormal);
 #endif
-    if (MODE != kParityOnly) stage_tables<AR>(&tab, a);
-    if constexpr (MODE != kParityOnly && kPacked<AR, D>) {
+    if (MODE != kParityOnly) stage_glibc_tables(&tab, a.gglibc);
+    if constexpr (MODE != kParityOnly && kPacked<D>) {
         if (a.finite && sld(a.finite)) {  // kernel-uniform: one of the two bodies runs
-            check_block<D, MODE, NT, AR, true>(a, bx, by, per, tab, hb);
+            check_block<D, MODE, NT, true>(a, bx, by, per, tab, hb);
             return;
         }
     }
-    check_block<D, MODE, NT, AR, false>(a, bx, by, per, tab, hb);
+    check_block<D, MODE, NT, false>(a, bx, by, per, tab, hb);
 }
 
 template <bool INIT, bool NT>
@@ -520,7 +467,7 @@ __device__ __forceinline__ void check_narrow_block(const CheckArgs &a, const Gli
     }
     double out[D];
     check_strict_packed<D, FIN ? kClampFinite : kClampFull>(m, out, hb + (threadIdx.x >> 6) * kPackWaveDoubles, tab,
-                                                            Arith<kStrict>::regs());
+                                                            GlibcK::pinned());
     const double s = sb ? -1.0 : 1.0;
     if (valid && act) {
 #pragma unroll
@@ -610,7 +557,7 @@ __device__ __forceinline__ void iter_block(const IterArgs &a, unsigned bx, unsig
         a.active[f] = 0;
     }
     if (!wave_any(act)) return;
-    const auto K = Arith<kStrict>::regs();
+    const auto K = GlibcK::pinned();
     const uint32_t b8 = (uint32_t)f * 8u;
     uint32_t bad = 0;
     for (int j = 0; j < a.g.per; ++j, ci += nsub) {
@@ -717,7 +664,7 @@ __device__ __forceinline__ void resident_loop(const ResArgs &a, int f, double *m
                                               const GlibcTablesBP &tab, double *wb) {
     const int tid = threadIdx.x;
     const size_t ld = a.ld;
-    const auto K = Arith<kStrict>::regs();
+    const auto K = GlibcK::pinned();
     // the first check of this thread (all of them when C <= kResThreads): its variables and
     // syndrome bit stay in registers across the iterations (D <= 6: within 128 VGPRs; above,
     // the indices would spill and are re-read from L1 instead)
@@ -813,40 +760,25 @@ __global__ void __launch_bounds__(kResThreads) __attribute__((amdgpu_waves_per_e
 // over the 1-D grid, in proportion to their counts) lets the dispatcher co-schedule
 // them on every CU, so the message stream of one hides under the arithmetic of the
 // other.
-// Occupancy floors (amdgpu_waves_per_eu, MI355X, scripts/exp_build.sh):
-//   exact box-plus (QR_FUSED_WAVES, 6 waves/SIMD = 80 VGPRs): 3.09 ms per launch vs
-//     3.14 (5 waves) / 3.26 (4 waves);
-//   exp domain (QR_FUSED_EPS_WAVES, 5 waves = 96 VGPRs, no spill): 2.73 ms vs 3.21
-//     (6 waves, 80 B spilled per lane inside the loop) / 2.94 (4 waves).
-//   strict box-plus (QR_FUSED_STRICT_WAVES, 4 waves = 128 VGPRs): 5.56 ms vs 5.68 (5
-//     waves, 96 VGPRs); issue-bound on fp64 VALU (the F and B chains evaluated side by
-//     side for more ILP: no gain).
-#ifndef QR_FUSED_WAVES
-#define QR_FUSED_WAVES 6
-#endif
-#ifndef QR_FUSED_EPS_WAVES
-#define QR_FUSED_EPS_WAVES 5
-#endif
+// Occupancy floor (amdgpu_waves_per_eu, MI355X, scripts/exp_build.sh): 4 waves/SIMD = 128
+// VGPRs, 5.56 ms per launch vs 5.68 at 5 waves (96 VGPRs); issue-bound on fp64 VALU (the F and
+// B chains evaluated side by side for more ILP: no gain).
 #ifndef QR_FUSED_STRICT_WAVES
 #define QR_FUSED_STRICT_WAVES 4
 #endif
-template <int AR>
-struct FusedWaves {
-    static constexpr int value = AR == kStrict ? QR_FUSED_STRICT_WAVES : AR == kEps ? QR_FUSED_EPS_WAVES : QR_FUSED_WAVES;
-};
 
-template <int D, int MODE, bool NT, int AR>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FusedWaves<AR>::value, 8)))
+template <int D, int MODE, bool NT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QR_FUSED_STRICT_WAVES, 8)))
 k_fused(CheckArgs ca, VarArgs va, unsigned nb_check, unsigned nb_total) {
-    __shared__ typename Arith<AR>::Tab tab;
-    __shared__ double hb[PackLds<AR>::doubles];
+    __shared__ GlibcTablesBP tab;
+    __shared__ double hb[kPackLdsDoubles];
     const unsigned b = blockIdx.x;
     const unsigned c0 = (unsigned)(((uint64_t)b * nb_check) / nb_total);
     const unsigned c1 = (unsigned)(((uint64_t)(b + 1) * nb_check) / nb_total);
     if (c1 > c0) {  // block-uniform branch
         if (!frames_block_live(ca.acount, c0 / ca.nbx, ca.g.lft)) return;
-        stage_tables<AR>(&tab, ca);
-        check_block<D, MODE, NT, AR>(ca, c0 % ca.nbx, c0 / ca.nbx, ca.g.per, tab, hb);
+        if (MODE != kParityOnly) stage_glibc_tables(&tab, ca.gglibc);
+        check_block<D, MODE, NT>(ca, c0 % ca.nbx, c0 / ca.nbx, ca.g.per, tab, hb);
     } else {
         const unsigned vi = b - c0;
         if (!frames_block_live(va.acount, vi / va.nbx, va.g.lft)) return;
@@ -867,10 +799,10 @@ k_fused(CheckArgs ca, VarArgs va, unsigned nb_check, unsigned nb_total) {
 // (decoder.pyx:322-369: the same box-plus operands in the same order per output.)
 constexpr int kMaxTemplDeg = 16;
 
-template <int MODE, int AR>
+template <int MODE>
 __global__ void __launch_bounds__(256) k_check_generic(CheckArgs a) {
-    __shared__ typename Arith<AR>::Tab tab;
-    if (MODE != kParityOnly) stage_tables<AR>(&tab, a);
+    __shared__ GlibcTablesBP tab;
+    if (MODE != kParityOnly) stage_glibc_tables(&tab, a.gglibc);
     const int ft = 1 << a.g.lft;
     const int nsub = 256 >> a.g.lft;
     const int ld = a.ld;
@@ -879,7 +811,7 @@ __global__ void __launch_bounds__(256) k_check_generic(CheckArgs a) {
     const int f = lane_frame(a.alist, a.acount, a.f_off, (int)(blockIdx.y << a.g.lft) + (threadIdx.x & (ft - 1)), live);
     const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> a.g.lft);
     if (!live || !a.active[f]) return;
-    const auto K = Arith<AR>::regs();
+    const auto K = GlibcK::pinned();
     const int64_t c0 = (int64_t)blockIdx.x * a.g.per * nsub + sub;
     const uint32_t b8 = (uint32_t)f * 8u;
     uint32_t bad = 0;
@@ -907,7 +839,7 @@ __global__ void __launch_bounds__(256) k_check_generic(CheckArgs a) {
         double F = msg(0, true);
         for (int i = 1; i <= d - 2; ++i) {
             *at_byte(fb + (size_t)(i - 1) * ld, b8) = F;  // F_{i-1}
-            F = Arith<AR>::bp(F, msg(i, true), tab, K);
+            F = box_plus_strict(F, msg(i, true), tab, K);
         }
         double Bn = msg(d - 1, true);
         if (MODE != kFirst) bad |= (par == 1u) ? 1u : 0u;
@@ -915,8 +847,8 @@ __global__ void __launch_bounds__(256) k_check_generic(CheckArgs a) {
         for (int i = d - 2; i >= 1; --i) {
             const double m = msg(i, false);  // before its edge's message is replaced
             const double Fi = *at_byte(fb + (size_t)(i - 1) * ld, b8);
-            *at_byte(row_ptr(a.c2v, sld(a.chk_edge + base + i), ld), b8) = s * Arith<AR>::bp(Fi, Bn, tab, K);
-            Bn = Arith<AR>::bp(Bn, m, tab, K);
+            *at_byte(row_ptr(a.c2v, sld(a.chk_edge + base + i), ld), b8) = s * box_plus_strict(Fi, Bn, tab, K);
+            Bn = box_plus_strict(Bn, m, tab, K);
         }
         *at_byte(row_ptr(a.c2v, sld(a.chk_edge + base), ld), b8) = s * Bn;
     }
@@ -1162,7 +1094,7 @@ static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base, size_
 
 // Runtime tuning knobs (qr_tune_set); defaults picked by scripts/tune.py on MI355X.
 struct Tuning {
-    std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3}, math{kStrict}, eps_max{40},
+    std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3},
         lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024}, var_pace{28},
         check_tail{4}, fused_iter{1}, iter_streams{2}, var_boost{4}, resident{1}, repack{1},
         repack_pct{75}, repack_lag0{1}, narrow{1};
@@ -1234,9 +1166,7 @@ struct Plan {
         a.g = make_geom(f1 - f0, g_tune.check_ft.load(), g_tune.check_per.load(), cls.n);
         const int64_t per_block = (int64_t)a.g.per * (256 >> a.g.lft);
         a.nbx = (unsigned)((cls.n + per_block - 1) / per_block);
-        a.gtab = code->d_mtab;
         a.gglibc = code->d_gtab;
-        a.eps_max = std::min<double>(g_tune.eps_max.load(), kEpsMax);
         a.fb = w.fb;
         a.fb_base = cls.fb_base;
         a.alist = a.acount = nullptr;
@@ -1278,12 +1208,6 @@ struct Plan {
         default: handled = false;                                                                            \
     }
 
-// Arithmetic of the check launches (knob math); parity-only sweeps need no tables.
-static int math_mode(int mode) {
-    const int m = g_tune.math.load();
-    return mode == kParityOnly ? kFast : (m == kFast || m == kEps) ? m : kStrict;
-}
-
 template <int MODE, bool NT>
 static int launch_check_class(const Plan &P, const DegreeClass &cls, const double *post_in, uint8_t *unsat, int f0,
                               int f1) {
@@ -1292,7 +1216,6 @@ static int launch_check_class(const Plan &P, const DegreeClass &cls, const doubl
         a.alist = P.w.alist;
         a.acount = P.count_of(f0);
     }
-    const int ar = math_mode(MODE);
     const dim3 grid2(a.nbx, (unsigned)((f1 - f0) >> a.g.lft));   // the plain 2-D grid
     dim3 grid = grid2;
     // knob check_tail (default 4; 0 = off; MI355X: +1 %): frame tile 0 is swept last with per / check_tail
@@ -1311,7 +1234,7 @@ static int launch_check_class(const Plan &P, const DegreeClass &cls, const doubl
                                 : std::string(),
                  P.s);
     // knob narrow (default 1): a repacked range of <= 64 columns, strict packed degrees
-    if (MODE == kNormal && P.narrow && P.compact && ar == kStrict && cls.degree >= 2 && cls.degree <= kPackMaxDeg &&
+    if (MODE == kNormal && P.narrow && P.compact && cls.degree >= 2 && cls.degree <= kPackMaxDeg &&
         f1 - f0 <= 64) {
         const dim3 gn((unsigned)((cls.n + kNarrowNodes - 1) / kNarrowNodes),
                       (unsigned)((f1 - f0 + kNarrowFrames - 1) / kNarrowFrames));
@@ -1330,9 +1253,7 @@ static int launch_check_class(const Plan &P, const DegreeClass &cls, const doubl
     }
 #define QR_CASE(DD)                                                                                   \
     case DD:                                                                                          \
-        if (ar == kStrict) k_check<DD, MODE, NT, kStrict><<<grid, 256, P.lds_pad, P.s>>>(a);          \
-        else if (ar == kEps) k_check<DD, MODE, NT, kEps><<<grid, 256, P.lds_pad, P.s>>>(a);           \
-        else k_check<DD, MODE, NT, kFast><<<grid, 256, P.lds_pad, P.s>>>(a);                          \
+        k_check<DD, MODE, NT><<<grid, 256, P.lds_pad, P.s>>>(a);                                     \
         break;
     bool handled = true;
     QR_DEG_SWITCH(cls.degree, QR_CASE, handled)
@@ -1340,8 +1261,7 @@ static int launch_check_class(const Plan &P, const DegreeClass &cls, const doubl
     if (!handled) {  // the runtime-degree kernel decodes its frame tile from blockIdx.y: 2-D grid only
         a.nmain = 0;
         a.per_t = a.g.per;
-        if (ar == kStrict) k_check_generic<MODE, kStrict><<<grid2, 256, 0, P.s>>>(a);
-        else k_check_generic<MODE, kFast><<<grid2, 256, 0, P.s>>>(a);
+        k_check_generic<MODE><<<grid2, 256, 0, P.s>>>(a);
     }
     QR_LAUNCH_CHECK();
     return QR_OK;
@@ -1399,7 +1319,6 @@ static int launch_var(const Plan &P, int f0, int f1, int32_t *finite = nullptr, 
 template <int MODE, bool NT>
 static int launch_fused_nt(const Plan &P, const DegreeClass &cls, uint8_t *unsat, int cf0, int cf1, int vf0, int vf1) {
     CheckArgs ca = P.check_args(cls, P.post, unsat, cf0, cf1);
-    const int ar = math_mode(MODE);
     VarArgs va = P.var_args(vf0, vf1);
     if (P.compact) {
         ca.alist = va.alist = P.w.alist;
@@ -1413,12 +1332,7 @@ static int launch_fused_nt(const Plan &P, const DegreeClass &cls, uint8_t *unsat
         ProfScope ps(profiling_on() ? std::string("fused_d") + std::to_string(cls.degree) : std::string(), P.s);
 #define QR_CASE(DD)                                                                           \
     case DD:                                                                                  \
-        if (ar == kStrict)                                                                    \
-            k_fused<DD, MODE, NT, kStrict><<<nbc + nbv, 256, 0, P.s>>>(ca, va, nbc, nbc + nbv);  \
-        else if (ar == kEps)                                                                  \
-            k_fused<DD, MODE, NT, kEps><<<nbc + nbv, 256, 0, P.s>>>(ca, va, nbc, nbc + nbv);     \
-        else                                                                                  \
-            k_fused<DD, MODE, NT, kFast><<<nbc + nbv, 256, 0, P.s>>>(ca, va, nbc, nbc + nbv);    \
+        k_fused<DD, MODE, NT><<<nbc + nbv, 256, 0, P.s>>>(ca, va, nbc, nbc + nbv);            \
         break;
         QR_DEG_SWITCH(cls.degree, QR_CASE, handled)
 #undef QR_CASE
@@ -1894,7 +1808,7 @@ static int run_iter(const Plan &P, int max_it) {
 // workgroups' LDS per CU (so 16 waves of <= 128 VGPRs per CU) under the strict arithmetic.
 static size_t resident_lds(const qr_code *code) { return (size_t)(code->E + code->V) * sizeof(double); }
 static bool resident_code(const qr_code *code) {
-    return g_tune.resident.load() && math_mode(kNormal) == kStrict && code->classes.size() == 1 &&
+    return g_tune.resident.load() && code->classes.size() == 1 &&
            code->classes[0].degree >= 2 && code->classes[0].degree <= kPackMaxDeg &&
            code->classes[0].n == code->C && code->C <= INT32_MAX / kPackMaxDeg && code->V < INT32_MAX &&
            resident_lds(code) + kResStaticLds <= 80 * 1024;
@@ -1962,7 +1876,7 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     const int fin_e = fin_x > 999.0 ? 0 : 1000 - (int)std::ceil(fin_x);
     if (fin_e < 1) QR_HIP(hipMemsetAsync(P.w.acount + 2, 0, sizeof(int32_t), s));
     // the flag itself is computed by the first variable sweep, which reads every LAPPR anyway
-    int32_t *fin_flag = (fin_e >= 1 && g_tune.math.load() == kStrict) ? P.w.acount + 2 : nullptr;
+    int32_t *fin_flag = fin_e >= 1 ? P.w.acount + 2 : nullptr;
     // decoder.pyx:400-405: the input itself may already satisfy the syndrome.
     if ((rc = launch_checks<kParityOnly>(P, lappr, P.w.unsat, 0, ld))) return rc;
     if ((rc = launch_status(P, 0, ld, 0, 0, 0, P.w.unsat))) return rc;
@@ -1981,7 +1895,7 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     const int64_t half_blocks = (max_n + (int64_t)gh.per * (256 >> gh.lft) - 1) / ((int64_t)gh.per * (256 >> gh.lft)) *
                                 ((ld / 2) >> gh.lft);
     const bool split = sp >= 2 && ld % 512 == 0 && max_deg <= 16 && half_blocks >= g_tune.split_min_blocks.load();
-    const bool iter = !split && max_it > 0 && g_tune.fused_iter.load() && P.w.c2v2 && math_mode(kNormal) == kStrict;
+    const bool iter = !split && max_it > 0 && g_tune.fused_iter.load() && P.w.c2v2;
     if (iter) {
         if ((rc = run_iter(P, max_it))) return rc;
         // P(max_it + 1) was the parity sweep of the last posteriors; every frame still running stops
@@ -2086,7 +2000,6 @@ static int free_code(qr_code *c) {
     (void)hipFree(c->d_var_ptr);
     (void)hipFree(c->d_var_edge);
     (void)hipFree(c->d_var_slot);
-    (void)hipFree(c->d_mtab);
     (void)hipFree(c->d_gtab);
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -2151,11 +2064,9 @@ int qr_code_create(const int64_t *e_to_v, const int64_t *e_to_c, int64_t nv, int
         }
     }
     {
-        std::vector<MathTables> mt(1);
-        build_math_tables(&mt[0]);
         std::vector<GlibcTables> gt(1);
         build_glibc_tables(&gt[0]);
-        if ((rc = upload(&code->d_mtab, mt)) || (rc = upload(&code->d_gtab, gt))) {
+        if ((rc = upload(&code->d_gtab, gt))) {
             free_code(code);
             return rc;
         }
@@ -2203,8 +2114,7 @@ static std::atomic<int> *tune_knob(const char *name) {
         {"check_ft", &g_tune.check_ft},     {"check_per", &g_tune.check_per},
         {"var_ft", &g_tune.var_ft},         {"var_per", &g_tune.var_per},
         {"nt", &g_tune.nt},                 {"split", &g_tune.split},
-        {"math", &g_tune.math},             {"lds_pad_kb", &g_tune.lds_pad_kb},
-        {"eps_max", &g_tune.eps_max},       {"compact", &g_tune.compact},
+        {"lds_pad_kb", &g_tune.lds_pad_kb}, {"compact", &g_tune.compact},
         {"side", &g_tune.side},             {"demap_fast", &g_demap_fast},
         {"demap_hyp", &g_demap_hyp},        {"min_blocks", &g_tune.min_blocks},
         {"split_min_blocks", &g_tune.split_min_blocks},

@@ -475,7 +475,8 @@ __host__ __device__ __forceinline__ double h_strict(double s, const TT &T, const
 
 // decoder.pyx:41-45: (sgn(a)sgn(b) * min + h(|a+b|)) - h(|a-b|), each operation
 // rounded separately.  sgn(a)sgn(b)*min == copysign(min, a*b) up to the sign of an
-// exact zero and NaN cases, neither of which changes the result (fastmath.hpp).
+// exact zero and NaN cases, neither of which changes the result (a NaN operand makes
+// h(|a+-b|) NaN; a zero min adds a zero to h >= 0).
 // QR_STRICT_MAXMIN: the two h are taken at t+ = |a|+|b| and t- = ||a|-|b|| (the same
 // two values: |a+b| = t+ and |a-b| = t- when a*b >= 0, swapped otherwise, exactly, also
 // for zeros, infinities and NaN) so that each call site sees one population (t+ mostly

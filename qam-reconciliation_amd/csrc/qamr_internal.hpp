@@ -10,7 +10,7 @@
 
 #include "qamr.h"
 #include "qamr_math.hpp"
-#include "fastmath.hpp"
+#include "exp_table.hpp"
 #include "glibc_math.hpp"
 
 namespace qr {
@@ -101,7 +101,6 @@ struct qr_code {
     int32_t *d_var_slot = nullptr;
     std::vector<DegreeClass> classes;
     int64_t fb_rows = 0;  // rows of the F scratch (sum over runtime-degree classes)
-    qr::MathTables *d_mtab = nullptr;  // box-plus exp/log tables (fastmath.hpp)
     qr::GlibcTables *d_gtab = nullptr; // strict box-plus: glibc exp/log data (glibc_math.hpp)
     mutable qr::Scratch scratch;
     // two-stream schedule (decoder.hip run_split2): a second stream for the variable

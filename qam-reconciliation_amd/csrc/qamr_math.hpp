@@ -11,7 +11,7 @@
 
 #include <vector>
 
-#include "fastmath.hpp"
+#include "exp_table.hpp"
 #include "glibc_math.hpp"
 
 #define QR_HD __host__ __device__ __forceinline__
@@ -299,7 +299,7 @@ QR_HD double public_F_Y(const DemapTables &t, double y) {
     return res / t.M;
 }
 
-// exp(x) with the LDS tables of fastmath.hpp (<= ~1 ulp, like ocml/glibc exp): x = k ln2/256 + r,
+// exp(x) with the LDS table of exp_table.hpp (<= ~1 ulp, like ocml/glibc exp): x = k ln2/256 + r,
 // exp(x) = 2^(k>>8) 2^((k&255)/256) e^r.  Overflows to inf above ~709.8, underflows to 0;
 // NaN propagates.
 QR_HD double exp_fast(double x, const MathTables &T) {

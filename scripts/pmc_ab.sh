@@ -1,11 +1,11 @@
 #!/bin/bash
 # SQ counters of the dominant check kernel for several library builds (one rocprofv3
 # --pmc pass per counter group and build; decode_once.py = one short batched decode).
-#   LIBS="a.so b.so" [KERNEL='k_check<7, 1, true, 0>'] bash scripts/pmc_ab.sh
+#   LIBS="a.so b.so" [KERNEL='k_check<7, 1, true>'] bash scripts/pmc_ab.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-K=${KERNEL:-"k_check<7, 1, true, 0>"}
+K=${KERNEL:-"k_check<7, 1, true>"}
 G1=${G1:-"SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"}
 G2=${G2:-"SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_SALU"}
 G3=${G3:-"SQ_ACTIVE_INST_VALU2 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_THREAD_CYCLES_VALU SQ_CYCLES SQ_INSTS_VALU_TRANS_F64 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE"}

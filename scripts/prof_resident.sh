@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-ARGS="--workload reg1008_4pam --batch 1024 --steps 5 --warmup 1 --cpu-seconds 0 --no-roofline --no-alt --no-secondary"
+ARGS="--workload reg1008_4pam --batch 1024 --steps 5 --warmup 1 --cpu-seconds 0 --no-roofline --no-secondary"
 TAG=${PTAG:-r04}_resident TRACE_ARGS="$ARGS" PMC_ARGS="$ARGS" \
 PMC_GROUPS="FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE;SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_ACTIVE_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE" \
 bash scripts/profile_session.sh || exit 1

@@ -1,14 +1,13 @@
 """GPU parity tests of the decoder: libqamr (HIP, gfx950) against the reference's
 golden outputs and the oracle.  With the default (strict) arithmetic every output
 -- success flags, iteration counts, hard decisions and the final LAPPRs -- must be
-bit-exact (conftest.assert_bit_exact); the opt-in approximate arithmetics (math=1,
-2) within the north-star 1e-6 on LAPPRs (conftest.assert_llr_close)."""
+bit-exact (conftest.assert_bit_exact)."""
 import os
 
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, assert_bit_exact, assert_llr_close, golden
+from conftest import GOLDEN, assert_bit_exact, golden
 
 import oracle as O
 
@@ -202,13 +201,10 @@ def test_device_api_layout_and_properties(gpu):
     assert np.array_equal(s_p, s_h[perm]) and np.array_equal(i_p, i_h[perm]) and np.array_equal(f_p, f_h[perm])
 
 
-def test_math_modes(gpu):
-    """Strict arithmetic (default, math=0) is bit-identical to the oracle also on frames
-    whose check inputs leave the exp domain (|LLR| in the hundreds and thousands, inf);
-    the approximate modes (math=1 table h, math=2 exp domain with per-lane fallback to
-    math=1 beyond eps_max) keep success/iterations/hard decisions exact and LAPPRs
-    within 1e-6.  Results never depend on which frames share a wavefront (permuting
-    frames permutes results bit for bit)."""
+def test_large_magnitude_inputs_bit_exact(gpu):
+    """The strict arithmetic (the only one) is bit-identical to the oracle also on frames
+    whose check inputs are large (|LLR| in the hundreds and thousands, inf).  Results never
+    depend on which frames share a wavefront (permuting frames permutes results bit for bit)."""
     from qamr import _lib, codes
 
     vid, cid = codes.regular_code(1008)
@@ -225,27 +221,15 @@ def test_math_modes(gpu):
     llr[big[20:], :30] *= 1e4                                 # a few huge inputs per frame
     llr[big[0], 5] = np.inf
     s2, i2, f2 = orc.decode_batch(llr, synd, 50)
-    assert _lib.tune_get("math") == 0  # the default
-    try:
-        res = {}
-        for mode in (0, 1, 2):
-            _lib.tune_set("math", mode)
-            s1, i1, f1 = dec.decode_batch(llr, synd, 50)
-            assert np.array_equal(s1, s2) and np.array_equal(i1, i2), mode
-            assert np.array_equal(f1 < 0, f2 < 0), mode
-            if mode == 0:
-                assert_bit_exact(f1, f2)
-            else:
-                assert_llr_close(f1, f2)
-            res[mode] = f1
-        perm = rng.permutation(B)
-        for mode in (0, 2):
-            _lib.tune_set("math", mode)
-            s_p, i_p, f_p = dec.decode_batch(llr[perm], synd[perm], 50)
-            assert np.array_equal(s_p, s2[perm]) and np.array_equal(i_p, i2[perm])
-            assert_bit_exact(f_p, res[mode][perm])
-    finally:
-        _lib.tune_set("math", 0)
+    with pytest.raises(_lib.QamrError):  # the approximate arithmetics are gone
+        _lib.tune_set("math", 1)
+    s1, i1, f1 = dec.decode_batch(llr, synd, 50)
+    assert np.array_equal(s1, s2) and np.array_equal(i1, i2)
+    assert_bit_exact(f1, f2)
+    perm = rng.permutation(B)
+    s_p, i_p, f_p = dec.decode_batch(llr[perm], synd[perm], 50)
+    assert np.array_equal(s_p, s2[perm]) and np.array_equal(i_p, i2[perm])
+    assert_bit_exact(f_p, f1[perm])
 
 
 def test_decode_device_graph_capture(gpu):
