@@ -94,7 +94,10 @@ QR_API int qr_code_info(const qr_code *code, int64_t *vnum, int64_t *cnum, int64
 
 /* ------------------------------------------------------------------ decode */
 /* Device workspace (bytes) for qr_decode_batch_device at leading dim ld and
- * max_iterations (edge messages E*ld fp64 + per-frame flags). */
+ * max_iterations (edge messages E*ld fp64 + per-frame flags; with tuning knob "repack" on
+ * (default) and ld % 512 == 0, plus the column-repack work set: posteriors, LAPPRs, syndrome
+ * bits and frame ids, (16V + C + 4)*ld bytes -- a workspace without it runs the same decode
+ * without the repack). */
 QR_API int qr_decode_workspace_size(const qr_code *code, int32_t ld, int32_t max_iterations, size_t *bytes);
 
 /* Batched Decoder._decode (decoder.pyx:391-436) of B independent frames.
@@ -106,10 +109,24 @@ QR_API int qr_decode_workspace_size(const qr_code *code, int32_t ld, int32_t max
  *   d_success[B] uint8, d_iters[B] int32: the (success, iterations) pair of
  *                          _decode for every frame (decoder.pyx:433,436).
  * Per-frame early termination; results per frame are identical to decoding
- * that frame alone. */
+ * that frame alone.
+ * Asynchronous: every launch is enqueued on `stream` (the two-stream schedule also on a
+ * library-owned second stream, forked from and joined back into `stream` by events) and the
+ * call returns without waiting for the GPU; every schedule decision that depends on the data
+ * (early termination, active-frame lists, column repack) is taken on the device, so the call
+ * is capturable into a HIP graph and the replay computes the same results. */
 QR_API int qr_decode_batch_device(const qr_code *code, int32_t B, int32_t ld, const double *d_lappr, const uint8_t *d_synd,
                            int32_t max_iterations, double *d_final, uint8_t *d_success, int32_t *d_iters,
                            void *d_workspace, size_t workspace_bytes, void *stream);
+
+/* Diagnostics of the column repack of the last qr_decode_batch_device that used this workspace
+ * (the same code, ld, max_iterations and workspace): out[0], out[1] = how many times the device
+ * repacked frame range 0 / 1 of the two-stream schedule, out[2], out[3] = the width each range
+ * ended at (0 repacks and width ld / 2 for a range never repacked, and for every decode that did
+ * not take the two-stream schedule).
+ * Synchronous device-to-host copy: call after the decode has completed. */
+QR_API int qr_decode_repack_stats(const qr_code *code, int32_t ld, int32_t max_iterations, const void *d_workspace,
+                                  size_t workspace_bytes, int32_t *out);
 
 /* Decoder.decode (decoder.pyx:441-455) for B frames from host memory,
  * frame-major: lappr[B][V], synd[B][C], final[B][V]. */

@@ -133,6 +133,14 @@ struct CheckArgs {
     // workgroup's time.  nmain = 0: the plain 2-D grid (nbx x frame tiles).
     unsigned nmain;
     int per_t;
+    // Column repack (run_split2): sel -> the range's RangeSel, or null.  Once the device has
+    // repacked the range (sel[kSelOn]) its posteriors and syndrome bits live in the work set
+    // (post_w, synd_w).  narrow: a narrow kernel is launched beside this one for the same range;
+    // the regular kernel then leaves when sel[kSelNarrow] is set, the narrow one when it is not.
+    const int32_t *sel;
+    const double *post_w;
+    const uint8_t *synd_w;
+    int narrow;
 };
 
 // One variable sweep over the frame columns [f_off, f_off + ny*ft).
@@ -154,7 +162,35 @@ struct VarArgs {
     int32_t *finite;
     double fin_bound;
     int fin_B;
+    const int32_t *sel;  // as CheckArgs: the range's RangeSel or null; work-set LAPPRs / posteriors
+    const double *lappr_w;
+    double *post_w;
+    int narrow;
 };
+
+// The state of one frame range of the two-stream schedule, in device memory (the workspace's
+// count block), read by every launch of that range and written only by k_repack_commit: whether
+// the range has moved to the repack work set, its width there (its running frames occupy the
+// first columns), whether the narrow kernels sweep it, and how many repacks it went through.
+enum RangeSelField { kSelOn = 0, kSelW = 1, kSelNarrow = 2, kSelRepacks = 3, kSelInts = 4 };
+
+// Kernel-uniform: the arrays a range's launch reads once the device has repacked the range.
+__device__ __forceinline__ void select_range(CheckArgs &a) {
+    if (a.sel && sld(a.sel + kSelOn)) {
+        a.post = a.post_w;
+        a.synd = a.synd_w;
+    }
+}
+__device__ __forceinline__ void select_range(VarArgs &a) {
+    if (a.sel && sld(a.sel + kSelOn)) {
+        a.lappr = a.lappr_w;
+        a.post = a.post_w;
+    }
+}
+// the regular sweep of a range the narrow kernels sweep (both are launched) leaves
+__device__ __forceinline__ bool swept_narrow(const int32_t *sel, int narrow) {
+    return narrow && sel && sld(sel + kSelNarrow);
+}
 
 // Active-frame compaction (converging operating points, decoder.pyx:431-433: frames stop
 // at their own iteration).  Without a list a sweep's lane p of the frame range is frame
@@ -380,6 +416,8 @@ template <int D, int MODE, bool NT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) k_check(CheckArgs a) {
     __shared__ GlibcTablesBP tab;
     __shared__ double hb[kPackLdsDoubles];
+    if (swept_narrow(a.sel, a.narrow)) return;  // kernel-uniform
+    select_range(a);
     unsigned bx = blockIdx.x, by = blockIdx.y;
     int per = a.g.per;
     if (a.nmain) {  // short-tail 1-D grid (block-uniform)
@@ -408,6 +446,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
 
 template <bool INIT, bool NT>
 __global__ void __launch_bounds__(256) k_var(VarArgs a) {
+    if (swept_narrow(a.sel, a.narrow)) return;  // kernel-uniform
+    select_range(a);
     if (a.gs) {  // capped grid: tile t = (bx fastest, by), the grid's blocks sweep a moving window
         unsigned ny = a.nby, stride = gridDim.x;
         if (a.boost > 1) {
@@ -480,6 +520,8 @@ template <int D>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) k_check_narrow(CheckArgs a) {
     __shared__ GlibcTablesBP tab;
     __shared__ double hb[4 * kPackWaveDoubles];
+    if (!sld(a.sel + kSelNarrow)) return;  // kernel-uniform: the regular kernel sweeps
+    select_range(a);
     if (!frames_block_live(a.acount, blockIdx.y * kNarrowFrames, 0)) return;  // block-uniform
     stage_glibc_tables(&tab, a.gglibc);
     if (a.finite && sld(a.finite)) check_narrow_block<D, true>(a, tab, hb);
@@ -487,6 +529,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
 }
 
 __global__ void __launch_bounds__(256) k_var_narrow(VarArgs a) {
+    if (!sld(a.sel + kSelNarrow)) return;  // kernel-uniform: the regular kernel sweeps
+    select_range(a);
     if (!frames_block_live(a.acount, blockIdx.y * kNarrowFrames, 0)) return;  // block-uniform
     bool live;
     const int p = (int)blockIdx.y * kNarrowFrames + (int)(threadIdx.x % kNarrowFrames);
@@ -802,6 +846,7 @@ constexpr int kMaxTemplDeg = 16;
 template <int MODE>
 __global__ void __launch_bounds__(256) k_check_generic(CheckArgs a) {
     __shared__ GlibcTablesBP tab;
+    select_range(a);
     if (MODE != kParityOnly) stage_glibc_tables(&tab, a.gglibc);
     const int ft = 1 << a.g.lft;
     const int nsub = 256 >> a.g.lft;
@@ -855,9 +900,12 @@ __global__ void __launch_bounds__(256) k_check_generic(CheckArgs a) {
     if (MODE != kFirst && bad) a.unsat[f] = 1;
 }
 
-__global__ void k_init_status(int B, int ld, uint8_t *active, uint8_t *success, int32_t *iters, int32_t *finite) {
+// rsel: the two ranges' RangeSel (widths w0, w1), initialised here for every schedule.
+__global__ void k_init_status(int B, int ld, uint8_t *active, uint8_t *success, int32_t *iters, int32_t *finite,
+                              int32_t *rsel, int w0, int w1) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f == 0) *finite = 1;
+    if (f < 2 * kSelInts) rsel[f] = (f % kSelInts == kSelW) ? (f < kSelInts ? w0 : w1) : 0;
     if (f >= ld) return;
     active[f] = (f < B) ? 1 : 0;
     if (f < B) {
@@ -866,15 +914,22 @@ __global__ void k_init_status(int B, int ld, uint8_t *active, uint8_t *success, 
     }
 }
 
+// The frame id of column f: f itself, or fid_w[f] once the range (RangeSel sel, or null) lives
+// in the repack work set.
+__device__ __forceinline__ const int32_t *range_fid(const int32_t *sel, const int32_t *fid_w) {
+    return (sel && sld(sel + kSelOn)) ? fid_w : nullptr;
+}
+
 // Frames in [f0, f1) whose posterior after sweep t satisfies the syndrome stop with
 // (success=1, iterations=t) (decoder.pyx:431-433, :402-405 for t = 0).  On the
 // final call every still-active frame stops with (0, max_iterations) (:435-436).
-// fid: the frame id of each column of a repacked range (null: column = frame).
+// sel / fid_w: see range_fid.
 __global__ void k_status(int f0, int f1, int t, int final_call, int32_t final_iters,
                          const uint8_t *__restrict__ unsat_t, uint8_t *active, uint8_t *success, int32_t *iters,
-                         const int32_t *__restrict__ fid) {
+                         const int32_t *sel, const int32_t *__restrict__ fid_w) {
     const int f = f0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= f1 || !active[f]) return;
+    const int32_t *fid = range_fid(sel, fid_w);
     const int id = fid ? fid[f] : f;
     if (!unsat_t[f]) {
         success[id] = 1;
@@ -892,16 +947,19 @@ __global__ void k_status(int f0, int f1, int t, int final_call, int32_t final_it
 // through LDS, one store per running frame.  STATUS: the status update of sweep t
 // (k_status, never the final call) is applied first, frame by frame, by the same thread:
 // one launch instead of two between the check sweeps of the two-stream schedule.
-// fid as k_status; hcount (or null): a host-mapped copy of the count, read by the host to
-// decide when to repack the range (run_split2).
+// sel / fid_w as k_status (a repacked range holds frames only in its first sel[kSelW] columns);
+// hcount (or null): a host-mapped copy of the count, which the host reads without waiting to
+// size the range's later launches (run_split2).
 template <bool STATUS>
 __global__ void __launch_bounds__(1024) k_compact(int f0, int f1, uint8_t *__restrict__ active,
                                                   int32_t *__restrict__ list, int32_t *__restrict__ count, int t,
                                                   const uint8_t *__restrict__ unsat_t, uint8_t *__restrict__ success,
-                                                  int32_t *__restrict__ iters, const int32_t *__restrict__ fid,
-                                                  int32_t *hcount) {
+                                                  int32_t *__restrict__ iters, const int32_t *sel,
+                                                  const int32_t *__restrict__ fid_w, int32_t *hcount) {
     __shared__ int wsum[16];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int32_t *fid = range_fid(sel, fid_w);
+    if (fid) f1 = min(f1, f0 + sld(sel + kSelW));
     int base = 0;  // running count (every thread keeps the same value)
     for (int c0 = f0; c0 < f1; c0 += 1024) {
         const int f = c0 + (int)threadIdx.x;
@@ -937,76 +995,164 @@ __global__ void __launch_bounds__(1024) k_compact(int f0, int f1, uint8_t *__res
 // scattered over the range: once most frames have stopped, every 8-byte message access of a
 // lane is a cache line of its own, and a launch over a few hundred frames costs as much as one
 // over the whole range (MI355X, 4-PAM 4.0 dB: 3.7 ms for 418 running frames of 2048, 1.6 ms
-// for 76).  The repack moves the running frames' columns (messages, LAPPRs, syndrome bits) to
-// the front of a fresh buffer set, so the range shrinks and the lanes read contiguous columns
-// again; fid[] maps each column back to its frame for the status writes and the final posteriors.
-// Each column copy moves the same bits: the decode's arithmetic is untouched.
+// for 76).  The repack moves the running frames' columns to the front of the range, so the
+// lanes read contiguous columns again.  Each column copy moves the same bits: the decode's
+// arithmetic is untouched.
+//
+// Everything is decided on the device, so the decode stays asynchronous and capturable: at
+// each decision point (before a range's variable sweep, on the variable stream) k_repack_rows
+// and k_repack_commit read the range's running-frame count (written by its last status
+// launch) and its RangeSel; when the running frames fill at most pct % of the range's width w,
+// the range moves to w' = max(64, count rounded up to 64):
+//   * messages: compacted in place in the workspace's c2v rows (the range's own columns);
+//   * posteriors, LAPPRs, syndrome bits: the first repack gathers them from the caller's arrays
+//     into the repack work set (same ld, the range's own columns), later ones compact them in
+//     place there; frames stopped since the last repack first hand their posteriors (in the
+//     work set) to the caller's output through fid;
+//   * fid[column] = the frame the column holds (-1: none), the list becomes the identity, the
+//     active flags follow the frames.
+// In-place compaction of a row (list ascending, so a column is only ever moved to a column at or
+// before it): chunks of columns in ascending order, all reads of a chunk complete before any of
+// its writes (one barrier); a later chunk reads only columns beyond every column written before.
+constexpr int kRepackThreads = 256;
+constexpr int kRepackPer = 8;  // columns per thread per chunk
+constexpr int kRepackChunk = kRepackThreads * kRepackPer;
 
-// dst[r][f0 + p] = src[r][list[f0 + p]] for p < *count (rows r < rows); each thread keeps
-// kGatherRows loads in flight
-constexpr int kGatherRows = 4;
+struct RepackArgs {
+    int f0, h, ld, pct;  // the range's first column and full width; repack threshold (percent)
+    int64_t E, V, C;
+    const int32_t *count;  // the range's running-frame count
+    int32_t *sel;          // its RangeSel
+    int32_t *list;         // active-frame list (absolute columns, list[f0 + p])
+    uint8_t *active;
+    double *c2v;
+    double *out_post;            // the caller's posterior output (frame f at column f)
+    const double *lappr_in;      // the caller's LAPPRs
+    const uint8_t *synd_in;      // the caller's syndrome bits
+    double *post_w, *lappr_w;    // the work set
+    uint8_t *synd_w;
+    int32_t *fid_w;
+};
+
+// The decision, taken identically by every workgroup of k_repack_rows and by k_repack_commit
+// (their inputs do not change between the two launches).
+__device__ __forceinline__ bool repack_go(const RepackArgs &r, int &cnt, int &w, int &w_new) {
+    cnt = sld(r.count);
+    w = sld(r.sel + kSelW);
+    if (w <= 64 || cnt <= 0 || (int64_t)cnt * 100 > (int64_t)w * r.pct) return false;
+    w_new = max(64, (cnt + 63) / 64 * 64);
+    return w_new < w;
+}
+
+// make every load of this thread complete, then the workgroup barrier: the loaded values are
+// in registers before any thread of the workgroup overwrites what they were loaded from
+__device__ __forceinline__ void loads_done_barrier() {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+}
+
 template <typename T>
-__global__ void k_gather_cols(int64_t rows, int f0, int ld, const int32_t *__restrict__ list,
-                              const int32_t *__restrict__ count, const T *__restrict__ src, T *__restrict__ dst) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= *count) return;
-    const int sc = list[f0 + p];
-    const int64_t gy = gridDim.y;
-    for (int64_t r = blockIdx.y; r < rows; r += kGatherRows * gy) {
-        T v[kGatherRows];
+__device__ __forceinline__ void compact_row(const T *src, T *dst, const int32_t *list, int f0, int cnt) {
+    for (int p0 = 0; p0 < cnt; p0 += kRepackChunk) {
+        T v[kRepackPer];
 #pragma unroll
-        for (int u = 0; u < kGatherRows; ++u) {
-            const int64_t rr = r + u * gy;
-            v[u] = rr < rows ? src[rr * ld + sc] : T(0);
+        for (int u = 0; u < kRepackPer; ++u) {
+            const int p = p0 + u * kRepackThreads + (int)threadIdx.x;
+            v[u] = p < cnt ? src[list[f0 + p]] : T(0);
         }
+        loads_done_barrier();
 #pragma unroll
-        for (int u = 0; u < kGatherRows; ++u) {
-            const int64_t rr = r + u * gy;
-            if (rr < rows) dst[rr * ld + f0 + p] = v[u];
+        for (int u = 0; u < kRepackPer; ++u) {
+            const int p = p0 + u * kRepackThreads + (int)threadIdx.x;
+            if (p < cnt) dst[f0 + p] = v[u];
         }
     }
 }
-// After the gathers: column f0 + p of the new set holds frame fid_src[list[f0 + p]] (p < count,
-// running) or nothing (count <= p < w: fid -1, stopped); the list becomes the identity.
-__global__ void k_repack_flags(int f0, int w, int32_t *__restrict__ list, const int32_t *__restrict__ count,
-                               const int32_t *__restrict__ fid_src, int32_t *__restrict__ fid_dst,
-                               uint8_t *__restrict__ active) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= w) return;
-    const int n = *count;
-    if (p < n) {
-        const int sc = list[f0 + p];
-        fid_dst[f0 + p] = fid_src ? fid_src[sc] : sc;
-        list[f0 + p] = f0 + p;
-        active[f0 + p] = 1;
-    } else {
-        fid_dst[f0 + p] = -1;
-        active[f0 + p] = 0;
+
+// Grid-stride over the rows: [0, E) messages, [E, E + V) posteriors, [E + V, E + 2V) LAPPRs,
+// [E + 2V, E + 2V + C) syndrome bytes.
+__global__ void __launch_bounds__(kRepackThreads) k_repack_rows(RepackArgs r) {
+    int cnt, w, w_new;
+    if (!repack_go(r, cnt, w, w_new)) return;  // kernel-uniform
+    const bool on = sld(r.sel + kSelOn) != 0;
+    const size_t ld = r.ld;
+    const int64_t rows = r.E + 2 * r.V + r.C;
+    for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+        if (row < r.E) {
+            double *q = r.c2v + (size_t)row * ld;
+            compact_row<double>(q, q, r.list, r.f0, cnt);
+        } else if (row < r.E + r.V) {
+            const int64_t v = row - r.E;
+            double *dst = r.post_w + (size_t)v * ld;
+            if (on) {
+                // frames stopped since the last repack: their posteriors to the output first
+                // (read before the compaction's barrier, which orders them before its writes)
+                for (int q = threadIdx.x; q < w; q += kRepackThreads) {
+                    const int id = r.fid_w[r.f0 + q];
+                    if (id >= 0 && !r.active[r.f0 + q]) r.out_post[(size_t)v * ld + id] = dst[r.f0 + q];
+                }
+            }
+            compact_row<double>(on ? dst : r.out_post + (size_t)v * ld, dst, r.list, r.f0, cnt);
+        } else if (row < r.E + 2 * r.V) {
+            const int64_t v = row - r.E - r.V;
+            double *dst = r.lappr_w + (size_t)v * ld;
+            compact_row<double>(on ? dst : r.lappr_in + (size_t)v * ld, dst, r.list, r.f0, cnt);
+        } else {
+            const int64_t c = row - r.E - 2 * r.V;
+            uint8_t *dst = r.synd_w + (size_t)c * ld;
+            compact_row<uint8_t>(on ? dst : r.synd_in + (size_t)c * ld, dst, r.list, r.f0, cnt);
+        }
     }
 }
-// final_post[r][fid[q]] = post[r][q] for the columns q of [f0, f0 + w) holding a frame that is no
-// longer running (ALL: every column holding a frame -- the end of the decode)
-__global__ void k_scatter_post(int64_t rows, int f0, int w, int ld, const int32_t *__restrict__ fid,
-                               const uint8_t *__restrict__ active, int all, const double *__restrict__ post,
-                               double *__restrict__ final_post) {
+
+// One workgroup after k_repack_rows: frame ids, list, active flags and the RangeSel.  allow_narrow:
+// the host launches the narrow kernels beside the regular ones for this range from here on.
+__global__ void __launch_bounds__(1024) k_repack_commit(RepackArgs r, int allow_narrow) {
+    int cnt, w, w_new;
+    const bool go = repack_go(r, cnt, w, w_new);
+    const bool on = sld(r.sel + kSelOn) != 0;
+    if (go) {
+        const int f0 = r.f0;
+        for (int p0 = 0; p0 < cnt; p0 += 1024) {
+            const int p = p0 + (int)threadIdx.x;
+            int id = 0;
+            if (p < cnt) {
+                const int sc = r.list[f0 + p];
+                id = on ? r.fid_w[sc] : sc;  // column = frame in the caller's arrays
+            }
+            loads_done_barrier();
+            if (p < cnt) {
+                r.fid_w[f0 + p] = id;
+                r.list[f0 + p] = f0 + p;
+                r.active[f0 + p] = 1;
+            }
+        }
+        for (int p = cnt + (int)threadIdx.x; p < w; p += 1024) {
+            r.fid_w[f0 + p] = -1;
+            r.active[f0 + p] = 0;
+        }
+    }
+    if (threadIdx.x == 0) {
+        const int on2 = (go || on) ? 1 : 0, w2 = go ? w_new : w;
+        if (go) {
+            r.sel[kSelOn] = 1;
+            r.sel[kSelW] = w2;
+            r.sel[kSelRepacks] += 1;
+        }
+        r.sel[kSelNarrow] = (on2 && w2 <= 64 && allow_narrow) ? 1 : 0;
+    }
+}
+
+// The end of the decode: every frame of a repacked range hands its posteriors to the output.
+__global__ void k_repack_output(int64_t rows, int f0, int ld, const int32_t *sel, const int32_t *__restrict__ fid_w,
+                                const double *__restrict__ post_w, double *__restrict__ out_post) {
+    if (!sld(sel + kSelOn)) return;  // kernel-uniform: never repacked (the output is the posteriors)
+    const int w = sld(sel + kSelW);
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= w) return;
-    const int id = fid[f0 + q];
-    if (id < 0 || (!all && active[f0 + q])) return;
-    const int64_t gy = gridDim.y;
-    for (int64_t r = blockIdx.y; r < rows; r += kGatherRows * gy) {
-        double v[kGatherRows];
-#pragma unroll
-        for (int u = 0; u < kGatherRows; ++u) {
-            const int64_t rr = r + u * gy;
-            v[u] = rr < rows ? post[rr * ld + f0 + q] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < kGatherRows; ++u) {
-            const int64_t rr = r + u * gy;
-            if (rr < rows) final_post[rr * ld + id] = v[u];
-        }
-    }
+    const int id = fid_w[f0 + q];
+    if (id < 0) return;
+    for (int64_t v = blockIdx.y; v < rows; v += gridDim.y) out_post[(size_t)v * ld + id] = post_w[(size_t)v * ld + f0 + q];
 }
 
 // ------------------------------------------------------------------ launch
@@ -1018,14 +1164,18 @@ struct DecodeWs {
     double *fb;      // F scratch of the runtime-degree classes (fb_rows rows of ld), or null
     int32_t *alist;  // active-frame lists of the frame ranges (ld entries)
     int32_t *acount; // their lengths: [0] range starting at frame 0, [1] the second half;
-                     // [2] the finite flag of the input LAPPRs (first variable sweep)
-    // the two column sets a repacked frame range lives in (k_gather_cols*, run_split2); present
-    // when the caller's workspace has room for them (ws_bytes counts them when knob repack is on)
-    struct RepackSet {
-        double *c2v, *post, *lappr;
+                     // [2] the finite flag of the input LAPPRs (first variable sweep);
+                     // [4, 12) the two ranges' RangeSel (rsel)
+    int32_t *rsel;
+    // the work set of the column repack (k_repack_rows, run_split2): posteriors, LAPPRs,
+    // syndrome bits and the frame id of each column of the repacked ranges (the messages are
+    // compacted in place); present when the caller's workspace has room for it (ws_bytes counts
+    // it when knob repack is on)
+    struct WorkSet {
+        double *post, *lappr;
         uint8_t *synd;
         int32_t *fid;
-    } rs[2];
+    } rs;
     bool repack;
 };
 
@@ -1044,8 +1194,8 @@ static size_t ws_base_bytes(const qr_code *code, int ld, int max_it) {
            align_up((size_t)ld * sizeof(int32_t), 256) + 256;
 }
 static size_t repack_set_bytes(const qr_code *code, int ld) {
-    return align_up((size_t)code->E * ld * sizeof(double), 256) + 2 * align_up((size_t)code->V * ld * sizeof(double), 256) +
-           align_up((size_t)code->C * ld, 256) + align_up((size_t)ld * sizeof(int32_t), 256);
+    return 2 * align_up((size_t)code->V * ld * sizeof(double), 256) + align_up((size_t)code->C * ld, 256) +
+           align_up((size_t)ld * sizeof(int32_t), 256);
 }
 static size_t ws_repack_bytes(const qr_code *code, int ld);  // after g_tune
 static size_t ws_bytes(const qr_code *code, int ld, int max_it) {
@@ -1072,22 +1222,19 @@ static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base, size_
     w.alist = (int32_t *)p;
     p += align_up((size_t)ld * sizeof(int32_t), 256);
     w.acount = (int32_t *)p;
+    w.rsel = w.acount + 4;
     p += 256;
     const size_t extra = ws_repack_bytes(code, ld);
     w.repack = extra > 0 && ws_size >= ws_base_bytes(code, ld, max_it) + extra;
-    for (auto &r : w.rs) {
-        r = DecodeWs::RepackSet{nullptr, nullptr, nullptr, nullptr, nullptr};
-        if (!w.repack) continue;
-        r.c2v = (double *)p;
-        p += align_up((size_t)code->E * ld * sizeof(double), 256);
-        r.post = (double *)p;
+    w.rs = DecodeWs::WorkSet{nullptr, nullptr, nullptr, nullptr};
+    if (w.repack) {
+        w.rs.post = (double *)p;
         p += align_up((size_t)code->V * ld * sizeof(double), 256);
-        r.lappr = (double *)p;
+        w.rs.lappr = (double *)p;
         p += align_up((size_t)code->V * ld * sizeof(double), 256);
-        r.synd = (uint8_t *)p;
+        w.rs.synd = (uint8_t *)p;
         p += align_up((size_t)code->C * ld, 256);
-        r.fid = (int32_t *)p;
-        p += align_up((size_t)ld * sizeof(int32_t), 256);
+        w.rs.fid = (int32_t *)p;
     }
     return w;
 }
@@ -1097,16 +1244,17 @@ struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3},
         lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024}, var_pace{28},
         check_tail{4}, fused_iter{1}, iter_streams{2}, var_boost{4}, resident{1}, repack{1},
-        repack_pct{75}, repack_lag0{1}, narrow{1};
+        repack_pct{75}, narrow{1};
 };
 static Tuning g_tune;
 
-// knob repack (default 1): the workspace carries the two column sets of the repacked ranges
-// when the two-stream schedule can run (ld % 512 == 0) and they take at most 96 GiB
+// knob repack (default 1): the workspace carries the work set of the repacked ranges when the
+// two-stream schedule can run (ld % 512 == 0) and the set takes at most 1/8 of the device's
+// memory (N=64800, ld=4096: 4.4 GB of 288 GB)
 static size_t ws_repack_bytes(const qr_code *code, int ld) {
     if (!g_tune.repack.load() || ld % 512) return 0;
-    const size_t b = 2 * repack_set_bytes(code, ld);
-    return b <= ((size_t)96 << 30) ? b : 0;
+    const size_t b = repack_set_bytes(code, ld);
+    return b <= code->mem_bytes / 8 ? b : 0;
 }
 
 // Frame tile ft (a divisor of ncols, <= ft_req) and nodes per thread.  Small problems (few
@@ -1143,11 +1291,16 @@ struct Plan {
     int lds_pad = 0;  // dynamic LDS reserved by each check workgroup (caps their CU residency)
     bool compact = false;  // sweeps of the main loop read the active-frame lists
     int var_pace = 0;      // variable sweeps: workgroups per 128 frames (0 = one per tile)
-    const int32_t *fid = nullptr;  // frame id of each column (a repacked range), or null
-    bool narrow = false;           // a repacked range: sweeps of <= 64 columns take the narrow kernels
+    // run_split2 with the device-steered column repack: every launch of a range carries the
+    // range's RangeSel (steer), the narrow kernels are launched beside the regular ones (narrow),
+    // parity-only sweeps read the active-frame lists too (list_parity: the final sweep)
+    bool steer = false;
+    bool narrow = false;
+    bool list_parity = false;
     int32_t *hcount = nullptr;     // host-mapped copy of the status launches' counts, or null
 
     const int32_t *count_of(int f0) const { return w.acount + (f0 == 0 ? 0 : 1); }
+    const int32_t *sel_of(int f0) const { return steer ? w.rsel + (f0 == 0 ? 0 : kSelInts) : nullptr; }
 
     CheckArgs check_args(const DegreeClass &cls, const double *post_in, uint8_t *unsat, int f0, int f1) const {
         CheckArgs a;
@@ -1173,6 +1326,10 @@ struct Plan {
         a.finite = w.acount + 2;
         a.nmain = 0;
         a.per_t = a.g.per;
+        a.sel = sel_of(f0);
+        a.post_w = w.rs.post;
+        a.synd_w = w.rs.synd;
+        a.narrow = 0;
         return a;
     }
     VarArgs var_args(int f0, int f1) const {
@@ -1196,6 +1353,10 @@ struct Plan {
         a.finite = nullptr;
         a.fin_bound = 0.0;
         a.fin_B = 0;
+        a.sel = sel_of(f0);
+        a.lappr_w = w.rs.lappr;
+        a.post_w = w.rs.post;
+        a.narrow = 0;
         return a;
     }
 };
@@ -1212,7 +1373,7 @@ template <int MODE, bool NT>
 static int launch_check_class(const Plan &P, const DegreeClass &cls, const double *post_in, uint8_t *unsat, int f0,
                               int f1) {
     CheckArgs a = P.check_args(cls, post_in, unsat, f0, f1);
-    if (P.compact && MODE != kParityOnly) {
+    if (P.compact && (MODE != kParityOnly || P.list_parity)) {
         a.alist = P.w.alist;
         a.acount = P.count_of(f0);
     }
@@ -1229,15 +1390,13 @@ static int launch_check_class(const Plan &P, const DegreeClass &cls, const doubl
         a.per_t = a.g.per / tail;
         grid = dim3((unsigned)(a.nmain + nbx_t), 1);
     }
-    ProfScope ps(profiling_on() ? std::string(MODE == kParityOnly ? "parity_d" : MODE == kFirst ? "check1_d" : "check_d") +
-                                      std::to_string(cls.degree)
-                                : std::string(),
-                 P.s);
-    // knob narrow (default 1): a repacked range of <= 64 columns, strict packed degrees
-    if (MODE == kNormal && P.narrow && P.compact && cls.degree >= 2 && cls.degree <= kPackMaxDeg &&
-        f1 - f0 <= 64) {
-        const dim3 gn((unsigned)((cls.n + kNarrowNodes - 1) / kNarrowNodes),
-                      (unsigned)((f1 - f0 + kNarrowFrames - 1) / kNarrowFrames));
+    // knob narrow (default 1): a range the device has repacked to <= 64 columns (strict packed
+    // degrees) is swept by the narrow kernel, launched beside the regular one; which of the two
+    // runs is read from the range's RangeSel on the device (run_split2)
+    if (MODE == kNormal && P.narrow && P.compact && a.sel && cls.degree >= 2 && cls.degree <= kPackMaxDeg) {
+        a.narrow = 1;
+        const dim3 gn((unsigned)((cls.n + kNarrowNodes - 1) / kNarrowNodes), (unsigned)(64 / kNarrowFrames));
+        ProfScope pn(profiling_on() ? "narrow_d" + std::to_string(cls.degree) : std::string(), P.s);
 #define QR_NARROW(DD)                                         \
     case DD:                                                  \
         k_check_narrow<DD><<<gn, 256, 0, P.s>>>(a);           \
@@ -1249,8 +1408,11 @@ static int launch_check_class(const Plan &P, const DegreeClass &cls, const doubl
         }
 #undef QR_NARROW
         QR_LAUNCH_CHECK();
-        return QR_OK;
     }
+    ProfScope ps(profiling_on() ? std::string(MODE == kParityOnly ? "parity_d" : MODE == kFirst ? "check1_d" : "check_d") +
+                                      std::to_string(cls.degree)
+                                : std::string(),
+                 P.s);
 #define QR_CASE(DD)                                                                                   \
     case DD:                                                                                          \
         k_check<DD, MODE, NT><<<grid, 256, P.lds_pad, P.s>>>(a);                                     \
@@ -1291,12 +1453,11 @@ static int launch_var(const Plan &P, int f0, int f1, int32_t *finite = nullptr, 
         a.alist = P.w.alist;
         a.acount = P.count_of(f0);
     }
-    if (!INIT && P.narrow && P.compact && f1 - f0 <= 64) {  // a repacked range (knob narrow)
-        const dim3 gn((unsigned)((P.code->V + kNarrowNodes - 1) / kNarrowNodes),
-                      (unsigned)((f1 - f0 + kNarrowFrames - 1) / kNarrowFrames));
+    if (!INIT && P.narrow && P.compact && a.sel) {  // beside the regular sweep (knob narrow, as the checks)
+        a.narrow = 1;
+        const dim3 gn((unsigned)((P.code->V + kNarrowNodes - 1) / kNarrowNodes), (unsigned)(64 / kNarrowFrames));
         k_var_narrow<<<gn, 256, 0, P.s>>>(a);
         QR_LAUNCH_CHECK();
-        return QR_OK;
     }
     dim3 grid(a.nbx, a.nby);
     // Paced sweep (the two-stream schedule's variable sweeps, Plan::var_pace): at most var_pace
@@ -1357,7 +1518,7 @@ static int launch_status(const Plan &P, int f0, int f1, int t, int final_call, i
     f1 = std::min(f1, P.B);
     if (f1 <= f0) return QR_OK;
     k_status<<<(f1 - f0 + 255) / 256, 256, 0, P.s>>>(f0, f1, t, final_call, final_iters, unsat_t, P.w.active,
-                                                     P.success, P.iters, P.fid);
+                                                     P.success, P.iters, P.sel_of(f0), P.w.rs.fid);
     QR_LAUNCH_CHECK();
     return QR_OK;
 }
@@ -1366,7 +1527,7 @@ static int launch_status(const Plan &P, int f0, int f1, int t, int final_call, i
 static int launch_compact(const Plan &P, int f0, int f1) {
     if (!P.compact) return QR_OK;
     k_compact<false><<<1, 1024, 0, P.s>>>(f0, f1, P.w.active, P.w.alist, const_cast<int32_t *>(P.count_of(f0)), 0,
-                                          nullptr, nullptr, nullptr, nullptr, nullptr);
+                                          nullptr, nullptr, nullptr, P.sel_of(f0), P.w.rs.fid, nullptr);
     QR_LAUNCH_CHECK();
     return QR_OK;
 }
@@ -1377,7 +1538,7 @@ static int launch_status_compact(const Plan &P, int f0, int f1, int t, const uin
     if (!P.compact) return launch_status(P, f0, f1, t, 0, 0, unsat_t);
     ProfScope ps("status", P.s);
     k_compact<true><<<1, 1024, 0, P.s>>>(f0, f1, P.w.active, P.w.alist, const_cast<int32_t *>(P.count_of(f0)), t,
-                                         unsat_t, P.success, P.iters, P.fid,
+                                         unsat_t, P.success, P.iters, P.sel_of(f0), P.w.rs.fid,
                                          P.hcount ? P.hcount + (f0 == 0 ? 0 : 1) : nullptr);
     QR_LAUNCH_CHECK();
     return QR_OK;
@@ -1475,12 +1636,11 @@ static int side_stream(const qr_code *code, hipStream_t *out) {
     return QR_OK;
 }
 
-// Host-mapped counts and the status event rings of the column repack (caller holds code->mu;
-// all or nothing).
-// A decode still finishing on another stream may write its counts while the next one starts:
-// every decode takes the next of kRepackSlots count pairs.
+// Host-mapped counts of the column repack (caller holds code->mu).  A decode still finishing on
+// another stream may write its counts while the next one starts: every decode takes the next of
+// kRepackSlots count pairs.
 constexpr int kRepackSlots = 32;
-static int repack_resources(const qr_code *code) {
+static int repack_counts(const qr_code *code) {
     if (!code->hc) {
         void *hp = nullptr, *dp = nullptr;
         hipError_t e = hipHostMalloc(&hp, 2 * kRepackSlots * sizeof(int32_t), hipHostMallocMapped);
@@ -1492,119 +1652,100 @@ static int repack_resources(const qr_code *code) {
         code->hc = (int32_t *)hp;
         code->hc_dev = (int32_t *)dp;
     }
-    if (!code->evs[0][0]) {
-        hipEvent_t ev[8] = {};
-        hipError_t e = hipSuccess;
-        for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
-        if (e != hipSuccess) {
-            for (auto x : ev)
-                if (x) (void)hipEventDestroy(x);
-            return set_error(QR_EDEVICE, "decode: repack events: %s", hipGetErrorString(e));
-        }
-        for (int i = 0; i < 8; ++i) code->evs[i / 4][i % 4] = ev[i];
-    }
     return QR_OK;
 }
 
-// One frame range of the two-stream schedule: columns [f0, f0 + w) of the caller's arrays
-// (set -1; the posteriors are the output itself) or of repack set w.rs[set].
-struct RangeLayout {
-    int f0, w, set;
-};
-
-static Plan layout_plan(const Plan &Q, const RangeLayout &L) {
-    Plan R = Q;
-    if (L.set >= 0) {
-        const auto &r = Q.w.rs[L.set];
-        R.lappr = r.lappr;
-        R.synd = r.synd;
-        R.post = r.post;
-        R.w.c2v = r.c2v;
-        R.fid = r.fid;
-        R.narrow = g_tune.narrow.load() != 0;
-        // the pacing spreads a full half's variable sweep over a full half's check launch (its
-        // paced length does not depend on the range's width); a repacked range's check launch
-        // is short, and so must be its variable sweep
-        R.var_pace = 0;
-    }
-    return R;
-}
-
-static unsigned gather_rows_grid(int64_t rows) { return (unsigned)std::min<int64_t>(rows, 2048); }
-
-// Move range L's running frames to the front of the other repack set (after its status launch,
-// on P.s); w_new >= the device count when the copy runs (counts only fall).
-static int repack_range(const Plan &P, RangeLayout &L, int w_new) {  // on P.s
+// A repack decision point of the range starting at column f0 (full width h), on P.s: the device
+// decides and, when it repacks, moves the columns (k_repack_rows) and updates the range's state
+// (k_repack_commit).
+static int launch_repack(const Plan &P, int f0, int h, int allow_narrow) {
     const qr_code *code = P.code;
-    const int ld = P.ld;
-    const int dst_set = L.set < 0 ? 0 : 1 - L.set;
-    const auto &dst = P.w.rs[dst_set];
-    const Plan S = layout_plan(P, L);  // the current arrays
-    const int32_t *count = P.count_of(L.f0);
+    RepackArgs r;
+    r.f0 = f0;
+    r.h = h;
+    r.ld = P.ld;
+    r.pct = std::clamp(g_tune.repack_pct.load(), 1, 90);
+    r.E = code->E;
+    r.V = code->V;
+    r.C = code->C;
+    r.count = P.count_of(f0);
+    r.sel = P.w.rsel + (f0 == 0 ? 0 : kSelInts);
+    r.list = P.w.alist;
+    r.active = P.w.active;
+    r.c2v = P.w.c2v;
+    r.out_post = P.post;
+    r.lappr_in = P.lappr;
+    r.synd_in = P.synd;
+    r.post_w = P.w.rs.post;
+    r.lappr_w = P.w.rs.lappr;
+    r.synd_w = P.w.rs.synd;
+    r.fid_w = P.w.rs.fid;
+    const int64_t rows = code->E + 2 * code->V + code->C;
     ProfScope ps("repack", P.s);
-    if (L.set >= 0) {  // frames stopped in this set hand their posteriors to the output first
-        k_scatter_post<<<dim3((unsigned)(L.w + 255) / 256, gather_rows_grid(code->V)), 256, 0, P.s>>>(
-            code->V, L.f0, L.w, ld, S.fid, P.w.active, 0, S.post, P.post);
-        QR_LAUNCH_CHECK();
-    }
-    const dim3 gx((unsigned)(w_new + 255) / 256);
-    k_gather_cols<double><<<dim3(gx.x, gather_rows_grid(code->E)), 256, 0, P.s>>>(code->E, L.f0, ld, P.w.alist, count,
-                                                                            S.w.c2v, dst.c2v);
+    k_repack_rows<<<(unsigned)std::min<int64_t>(rows, 4096), kRepackThreads, 0, P.s>>>(r);
     QR_LAUNCH_CHECK();
-    k_gather_cols<double><<<dim3(gx.x, gather_rows_grid(code->V)), 256, 0, P.s>>>(code->V, L.f0, ld, P.w.alist, count,
-                                                                            S.lappr, dst.lappr);
+    k_repack_commit<<<1, 1024, 0, P.s>>>(r, allow_narrow);
     QR_LAUNCH_CHECK();
-    k_gather_cols<uint8_t><<<dim3(gx.x, gather_rows_grid(code->C)), 256, 0, P.s>>>(code->C, L.f0, ld, P.w.alist, count,
-                                                                           S.synd, dst.synd);
-    QR_LAUNCH_CHECK();
-    k_repack_flags<<<gx, 256, 0, P.s>>>(L.f0, w_new, P.w.alist, count, S.fid, dst.fid, P.w.active);
-    QR_LAUNCH_CHECK();
-    L.set = dst_set;
-    L.w = w_new;
     return QR_OK;
 }
 
-// *finalized: the final parity check, status and output were issued here (a range was repacked).
+// *finalized: the final parity check, status and output were issued here (device-steered repack).
 static int run_split2(const Plan &P, int max_it, bool *finalized) {
     const qr_code *code = P.code;
+    // held while this decode ENQUEUES on the code's second stream and events; nothing here waits
+    // for the GPU
     std::lock_guard<std::mutex> lk(code->mu);
     *finalized = false;
     hipStream_t s2 = nullptr;
     if (int rc0 = side_stream(code, &s2)) return rc0;
     hipEvent_t fork = code->ev[0], cA = code->ev[1], cB = code->ev[2], vA = code->ev[3], vB = code->ev[4];
-    const int ld = P.ld, h = ld / 2;
-    // Column repack (knob repack; needs the workspace's repack sets and a stream that is not
-    // being captured, since the host reads the counts back): after a range's status launch, the
-    // host waits for that range's previous status launch (the GPU still has about an iteration
-    // of work queued), reads its count, and repacks the range when its running frames fill at
-    // most repack_pct % of its columns (default 75; MI355X, 4-PAM 4.0 dB, copies on the variable
-    // stream: 20.25-20.26 k frames/s at 75 %, 20.21-20.22 k at 85 %, 20.07-20.14 k at 65 %;
-    // copies on the check stream, another box: 20.32-20.34 k at 65 %, 20.20-20.34 k at 50 %,
-    // 19.91-20.10 k at 35 %, 19.55 k without the repack).
-    bool rp = P.compact && P.w.repack && g_tune.repack.load();
-    if (rp) {
+    const int ld = P.ld, h = ld / 2;  // ld % 512 == 0: both ranges are h columns wide
+    // Column repack (knob repack, default 1; needs the workspace's work set), decided on the device
+    // (k_repack_rows / k_repack_commit at every decision point).  The host only picks launch
+    // shapes, from the host-mapped counts it reads WITHOUT waiting (each is an upper bound of
+    // every later count of its range, since counts only fall): while no frame of a range has
+    // stopped it skips that range's decision launches (no cost at 3 dB), it sizes the sweeps'
+    // grids to the count, leaves a sparse range's variable sweep unpaced, and once the count is at
+    // most 64 launches the narrow kernels beside the regular ones and lets the device switch to
+    // them.  Under stream capture nothing can be read: every decision point is launched, grids keep
+    // the full width and the narrow kernels stay off -- the same results, a slower tail.
+    // MI355X, round 4 (host-decided repack, copies on the variable stream): 4-PAM 4.0 dB +5.7 %,
+    // 16-PAM 14.5 dB +2.5 %; threshold (knob repack_pct) 75 % best of 65 / 75 / 85.
+    const bool rp = P.compact && P.w.repack && g_tune.repack.load();
+    bool capturing = false;
+    {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        if (hipStreamIsCapturing(P.s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) rp = false;
+        if (hipStreamIsCapturing(P.s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) capturing = true;
     }
-    if (rp) {
-        if (int rc0 = repack_resources(code)) return rc0;
+    const bool hints = rp && !capturing;
+    if (hints) {
+        if (int rc0 = repack_counts(code)) return rc0;
     }
-    Plan Pb = P;  // status launches (P.s)
-    int32_t *hc = nullptr;
-    if (rp) {
+    Plan base = P;
+    base.steer = rp;
+    Plan Pb = base;  // status launches (P.s)
+    const int32_t *hc = nullptr;
+    if (hints) {
         const int slot = 2 * (int)(code->hc_gen++ % kRepackSlots);
+        code->hc[slot] = code->hc[slot + 1] = ld;
         hc = code->hc + slot;
         Pb.hcount = code->hc_dev + slot;
-        hc[0] = hc[1] = ld;
     }
-    Plan V = P;
+    auto stale = [&](int k) -> int { return hints ? *(volatile const int32_t *)(hc + k) : ld; };
+    const int pct = std::clamp(g_tune.repack_pct.load(), 1, 90);
+    // the grid width of range k's sweeps: covers every frame its list can still hold
+    auto cols = [&](int k) -> int { return hints ? std::clamp((stale(k) + 63) / 64 * 64, 64, h) : h; };
+    bool steering[2] = {false, false}, narrow_on[2] = {false, false};
+    Plan V = base;
     V.s = s2;
     V.var_pace = g_tune.var_pace.load();
-    Plan C = P;
+    Plan C = base;
     C.lds_pad = std::max(0, g_tune.lds_pad_kb.load()) * 1024;
-    RangeLayout L[2] = {{0, h, -1}, {h, ld - h, -1}};
-    int nstat[2] = {0, 0};
-    bool any_repack = false;
+    auto plan_for = [&](const Plan &Q, int k) {
+        Plan X = Q;
+        X.narrow = narrow_on[k];
+        return X;
+    };
     auto row = [&](int t) { return P.w.unsat + (size_t)t * ld; };
     // Knob side (default 1): the check sweeps of the small degree classes (DVB-S2: the one
     // degree-6 check) run on the variable stream right after the variable sweep they follow,
@@ -1619,74 +1760,51 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
         if (k != big) side_edges += code->classes[k].n * code->classes[k].degree;
     const bool side = g_tune.side.load() && code->classes.size() > 1 && side_edges * 8 <= code->E;
     auto checks_main = [&](int t, int k) {  // check sweep t >= 2 of range k on the check stream
-        const Plan Q = layout_plan(C, L[k]);
-        const int f0 = L[k].f0, f1 = L[k].f0 + L[k].w;
-        if (!side) return launch_checks<kNormal>(Q, Q.post, row(t - 1), f0, f1);
+        const Plan Q = plan_for(C, k);
+        const int f0 = k * h, f1 = f0 + cols(k);
+        if (!side) return launch_checks<kNormal>(Q, P.post, row(t - 1), f0, f1);
         const DegreeClass &cls = code->classes[big];
-        return P.nt ? launch_check_class<kNormal, true>(Q, cls, Q.post, row(t - 1), f0, f1)
-                    : launch_check_class<kNormal, false>(Q, cls, Q.post, row(t - 1), f0, f1);
+        return P.nt ? launch_check_class<kNormal, true>(Q, cls, P.post, row(t - 1), f0, f1)
+                    : launch_check_class<kNormal, false>(Q, cls, P.post, row(t - 1), f0, f1);
     };
     auto checks_side = [&](int t, int k) {  // the other classes of check sweep t, on V.s
         if (!side) return (int)QR_OK;
-        const Plan Q = layout_plan(V, L[k]);
-        return launch_checks<kNormal>(Q, Q.post, row(t - 1), L[k].f0, L[k].f0 + L[k].w, big);
+        const Plan Q = plan_for(V, k);
+        return launch_checks<kNormal>(Q, P.post, row(t - 1), k * h, k * h + cols(k), big);
     };
-    int pending[2] = {0, 0};  // per range: the repacked width to apply before its next variable sweep
-    std::function<int(int)> decide_fn;
+    // range k's variable sweep, preceded by its repack decision point (the status launch it waits
+    // for wrote the count the device decides on); the copies run under the other range's check
+    // launch
     auto var_sweep = [&](int k) {
-        if (int rc0 = decide_fn(k)) return rc0;
-        if (pending[k]) {
-            if (int rc0 = repack_range(V, L[k], pending[k])) return rc0;
-            pending[k] = 0;
+        const int f0 = k * h;
+        if (rp) {
+            const int sc = stale(k);
+            if (capturing || steering[k] || sc < h) {
+                steering[k] = true;
+                if (hints && sc <= 64 && g_tune.narrow.load()) narrow_on[k] = true;
+                if (int rc0 = launch_repack(V, f0, h, narrow_on[k] ? 1 : 0)) return rc0;
+            }
         }
-        return launch_var<false>(layout_plan(V, L[k]), L[k].f0, L[k].f0 + L[k].w);
+        Plan Q = plan_for(V, k);
+        // the pacing spreads a full range's variable sweep over a full range's check launch; a
+        // sparse range's check launch is short, and so must be its variable sweep
+        if (hints && (int64_t)stale(k) * 100 <= (int64_t)h * pct) Q.var_pace = 0;
+        return launch_var<false>(Q, f0, f0 + cols(k));
     };
-    // status of sweep ts of range k (+ compaction), then the repack decision; the repack itself
-    // is enqueued on the variable stream right before range k's next variable sweep (it waits
-    // for this status through the event that sweep waits on), so its copies run under the
-    // other range's check launch instead of on the check stream
     auto status = [&](int k, int ts) -> int {
-        int rc0 = launch_status_compact(layout_plan(Pb, L[k]), L[k].f0, L[k].f0 + L[k].w, ts, row(ts));
-        if (rc0 || !rp) return rc0;
-        QR_HIP(hipEventRecord(code->evs[k][nstat[k] % 4], P.s));
-        ++nstat[k];
-        return QR_OK;
+        return launch_status_compact(Pb, k * h, (k + 1) * h, ts, row(ts));
     };
-    // The repack decision for range k, made right before its variable sweep is enqueued (the
-    // repack runs there).  Until the range's count first falls, the host reads the count of the
-    // status launch before the latest one (the GPU is an iteration ahead of that point: no
-    // bubble); from then on (knob repack_lag0, default 1) the latest one -- the variable stream
-    // waits for that status anyway, and the check stream still has the other launches queued.
-    int last_cnt[2] = {-1, -1};
-    bool conv[2] = {false, false};
-    auto decide = [&](int k) -> int {
-        if (!rp || nstat[k] < 1 || L[k].w <= 64) return QR_OK;
-        // the two ranges converge together: a fall seen in either switches both
-        const bool lag0 = (conv[0] || conv[1]) && g_tune.repack_lag0.load();
-        if (!lag0 && nstat[k] < 2) return QR_OK;
-        QR_HIP(hipEventSynchronize(code->evs[k][(nstat[k] - (lag0 ? 1 : 2)) % 4]));
-        const int cnt = *(volatile int32_t *)(hc + k);
-        if (last_cnt[k] >= 0 && cnt < last_cnt[k]) conv[k] = true;  // (a lag-0 read never precedes a lag-1 one)
-        last_cnt[k] = cnt;
-        if (cnt < 0 || (int64_t)cnt * 100 > (int64_t)L[k].w * std::clamp(g_tune.repack_pct.load(), 1, 90)) return QR_OK;
-        const int w_new = std::max(64, (cnt + 63) / 64 * 64);
-        if (w_new >= L[k].w) return QR_OK;
-        any_repack = true;
-        pending[k] = w_new;
-        return QR_OK;
-    };
-    decide_fn = decide;
     int rc;
     QR_HIP(hipEventRecord(fork, P.s));
     QR_HIP(hipStreamWaitEvent(V.s, fork, 0));
     if ((rc = launch_checks<kFirst>(C, P.post, row(0), 0, h))) return rc;
     QR_HIP(hipEventRecord(cA, P.s));
     for (int t = 1; t <= max_it; ++t) {
-        // every frame of both ranges has stopped (counts only fall; the host's copies lag): the
-        // remaining iterations would sweep nothing -- leave the loop with both ranges at a
+        // every frame of both ranges has stopped (the counts the host sees lag, but only fall):
+        // the remaining iterations would sweep nothing -- leave the loop with both ranges at a
         // status boundary (B after S_B(t-1), A after S_A(t-1)); the final parity check and
         // status below then find no running frame
-        if (rp && t >= 3 && *(volatile int32_t *)(hc + 0) == 0 && *(volatile int32_t *)(hc + 1) == 0) break;
+        if (hints && t >= 3 && stale(0) == 0 && stale(1) == 0) break;
         QR_HIP(hipStreamWaitEvent(V.s, cA, 0));
         if ((rc = var_sweep(0))) return rc;
         if (t < max_it && (rc = checks_side(t + 1, 0))) return rc;
@@ -1713,20 +1831,21 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
     // join: everything after (final parity check, status) follows both sweeps (vB follows cB)
     QR_HIP(hipStreamWaitEvent(P.s, vA, 0));
     QR_HIP(hipStreamWaitEvent(P.s, vB, 0));
-    if (!any_repack) return QR_OK;
-    // decoder.pyx:424-436 per range in its own columns: the parity of the last posteriors, the
-    // final status, then every frame of a repacked set hands its posteriors to the output
+    if (!rp) return QR_OK;
+    // decoder.pyx:424-436 per range, wherever its frames live: the parity of the last posteriors
+    // of its running frames (the lists), the final status, then every frame of a repacked range
+    // hands its posteriors to the output
     uint8_t *unsat_last = row(max_it);
+    Plan F = base;
+    F.list_parity = true;
     for (int k = 0; k < 2; ++k) {
-        const Plan R = layout_plan(P, L[k]);
-        const int f0 = L[k].f0, f1 = L[k].f0 + L[k].w;
-        if ((rc = launch_checks<kParityOnly>(R, R.post, unsat_last, f0, f1))) return rc;
-        if ((rc = launch_status(R, f0, f1, max_it, 1, max_it, unsat_last))) return rc;
-        if (L[k].set >= 0) {
-            k_scatter_post<<<dim3((unsigned)(L[k].w + 255) / 256, gather_rows_grid(code->V)), 256, 0, P.s>>>(
-                code->V, f0, L[k].w, ld, R.fid, P.w.active, 1, R.post, P.post);
-            QR_LAUNCH_CHECK();
-        }
+        const int f0 = k * h;
+        if ((rc = launch_checks<kParityOnly>(F, P.post, unsat_last, f0, f0 + cols(k)))) return rc;
+        if ((rc = launch_status(F, f0, f0 + h, max_it, 1, max_it, unsat_last))) return rc;
+        ProfScope ps("repack", P.s);
+        k_repack_output<<<dim3((unsigned)(h + 255) / 256, (unsigned)std::min<int64_t>(code->V, 2048)), 256, 0, P.s>>>(
+            code->V, f0, ld, F.sel_of(f0), P.w.rs.fid, P.w.rs.post, P.post);
+        QR_LAUNCH_CHECK();
     }
     *finalized = true;
     return QR_OK;
@@ -1808,10 +1927,13 @@ static int run_iter(const Plan &P, int max_it) {
 // workgroups' LDS per CU (so 16 waves of <= 128 VGPRs per CU) under the strict arithmetic.
 static size_t resident_lds(const qr_code *code) { return (size_t)(code->E + code->V) * sizeof(double); }
 static bool resident_code(const qr_code *code) {
+    // 80 KiB keeps two workgroups per gfx950 CU (160 KiB); never more than the device lets a
+    // workgroup take (otherwise the fused-iteration or flat schedule runs the code)
+    const size_t lds_cap = std::min<size_t>(80 * 1024, code->lds_per_block);
     return g_tune.resident.load() && code->classes.size() == 1 &&
            code->classes[0].degree >= 2 && code->classes[0].degree <= kPackMaxDeg &&
            code->classes[0].n == code->C && code->C <= INT32_MAX / kPackMaxDeg && code->V < INT32_MAX &&
-           resident_lds(code) + kResStaticLds <= 80 * 1024;
+           resident_lds(code) + kResStaticLds <= lds_cap;
 }
 
 static int run_resident(const qr_code *code, int B, int ld, const double *lappr, const uint8_t *synd, int max_it,
@@ -1868,7 +1990,8 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
     const int64_t rows = (int64_t)(max_it > 0 ? max_it : 0) + 2;  // no int overflow at INT_MAX
     int rc;
     QR_HIP(hipMemsetAsync(P.w.unsat, 0, (size_t)rows * ld, s));
-    k_init_status<<<(ld + 255) / 256, 256, 0, s>>>(B, ld, P.w.active, success, iters, P.w.acount + 2);
+    k_init_status<<<(ld + 255) / 256, 256, 0, s>>>(B, ld, P.w.active, success, iters, P.w.acount + 2, P.w.rsel, ld / 2,
+                                                   ld - ld / 2);
     QR_LAUNCH_CHECK();
     // the strict arithmetic's finite flag: bound 2^e with e = 1000 - (max_it + 2) log2(dv_max + 1)
     // (in double, clamped before the cast: max_it may be as large as INT_MAX)
@@ -2003,9 +2126,6 @@ static int free_code(qr_code *c) {
     (void)hipFree(c->d_gtab);
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
-    for (auto &r : c->evs)
-        for (auto &e : r)
-            if (e) (void)hipEventDestroy(e);
     if (c->hc) (void)hipHostFree(c->hc);
     if (c->s2) (void)hipStreamDestroy(c->s2);
     delete c;
@@ -2047,6 +2167,14 @@ int qr_code_create(const int64_t *e_to_v, const int64_t *e_to_c, int64_t nv, int
     code->max_dv = max_dv;
     code->device = device;
     code->scratch.device = device;
+    {
+        size_t mem = 0;
+        int lds = 0;
+        if (hipDeviceTotalMem(&mem, device) != hipSuccess) mem = 0;
+        if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess) lds = 0;
+        code->mem_bytes = mem;
+        code->lds_per_block = (size_t)(lds > 0 ? lds : 0);
+    }
     int rc = QR_OK;
     if ((rc = upload(&code->d_chk_ptr, chk_ptr)) || (rc = upload(&code->d_chk_edge, chk_edge)) ||
         (rc = upload(&code->d_chk_var, chk_var)) || (rc = upload(&code->d_var_ptr, var_ptr)) ||
@@ -2121,7 +2249,7 @@ static std::atomic<int> *tune_knob(const char *name) {
         {"var_pace", &g_tune.var_pace},     {"check_tail", &g_tune.check_tail}, {"var_boost", &g_tune.var_boost},
         {"fused_iter", &g_tune.fused_iter}, {"iter_streams", &g_tune.iter_streams},
         {"resident", &g_tune.resident},   {"repack", &g_tune.repack},
-        {"repack_pct", &g_tune.repack_pct}, {"repack_lag0", &g_tune.repack_lag0}, {"narrow", &g_tune.narrow},
+        {"repack_pct", &g_tune.repack_pct}, {"narrow", &g_tune.narrow},
     };
     const std::string n = name ? name : "";
     for (const auto &k : knobs)
@@ -2160,6 +2288,22 @@ int qr_decode_workspace_size(const qr_code *code, int32_t ld, int32_t max_it, si
     if (!code || !bytes) return set_error(QR_EVALUE, "null argument");
     if (ld <= 0 || ld % kWave) return set_error(QR_EVALUE, "ld must be a positive multiple of 64");
     *bytes = ws_bytes(code, ld, max_it);
+    return QR_OK;
+}
+
+int qr_decode_repack_stats(const qr_code *code, int32_t ld, int32_t max_it, const void *ws, size_t ws_size,
+                           int32_t *out) {
+    if (!code || !ws || !out) return set_error(QR_EVALUE, "null argument");
+    if (ld <= 0 || ld % kWave) return set_error(QR_EVALUE, "ld must be a positive multiple of 64");
+    if (ws_size < ws_base_bytes(code, ld, max_it)) return set_error(QR_EVALUE, "workspace too small");
+    const DecodeWs w = carve(code, ld, max_it, const_cast<void *>(ws), ws_size);
+    int32_t sel[2 * kSelInts];
+    DeviceGuard dg(code->device);
+    QR_HIP(hipMemcpy(sel, w.rsel, sizeof(sel), hipMemcpyDeviceToHost));
+    for (int k = 0; k < 2; ++k) {
+        out[k] = sel[k * kSelInts + kSelRepacks];
+        out[2 + k] = sel[k * kSelInts + kSelW];
+    }
     return QR_OK;
 }
 

@@ -92,6 +92,8 @@ struct qr_code {
     int64_t E = 0, V = 0, C = 0;
     int32_t max_dc = 0, max_dv = 0;
     int device = 0;
+    size_t mem_bytes = 0;       // the device's memory (bounds the optional repack work set)
+    size_t lds_per_block = 0;   // LDS a workgroup may take (the frame-resident decode needs it)
     // CSR, int32 (E < 2^31): per check, edge ids ascending and their variables;
     // per variable, edge ids ascending.
     int32_t *d_chk_ptr = nullptr, *d_chk_edge = nullptr, *d_chk_var = nullptr;
@@ -110,10 +112,11 @@ struct qr_code {
     mutable hipStream_t s2 = nullptr;
     mutable hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     // column repack of the two-stream schedule: host-mapped copies of the two ranges' running-
-    // frame counts and a ring of events per range after its status launches (created on first use)
+    // frame counts (created on first use).  The host only ever reads them without waiting, as
+    // upper bounds of the counts still to come (counts only fall), to size launches; every
+    // decision that changes a result is taken on the device.
     mutable int32_t *hc = nullptr, *hc_dev = nullptr;  // kRepackSlots pairs, one per decode in turn
     mutable unsigned hc_gen = 0;
-    mutable hipEvent_t evs[2][4] = {};
 };
 
 struct qr_demap {

@@ -41,6 +41,7 @@ SIGNATURES = {
     "qr_code_info": [vp, P(i64), P(i64), P(i64), P(i32), P(i32)],
     "qr_decode_workspace_size": [vp, i32, i32, P(C.c_size_t)],
     "qr_decode_batch_device": [vp, i32, i32, vp, vp, i32, vp, vp, vp, vp, C.c_size_t, vp],
+    "qr_decode_repack_stats": [vp, i32, i32, vp, C.c_size_t, P(C.c_int32)],
     "qr_decode_host": [vp, i32, vp, vp, i32, vp, vp, vp],
     "qr_check_lappr_host": [vp, vp, vp, vp, vp],
     "qr_check_word_host": [vp, vp, vp, vp, vp],

@@ -241,6 +241,22 @@ class Decoder:
             C.c_void_p(stream.cuda_stream)), "decode_device")
         return final_fi, success, iters
 
+    def repack_stats(self, ld: int, max_iterations: int, stream=None):
+        """Column repack of the last decode_device on ``stream`` (same ld, max_iterations):
+        ((repacks of range 0, repacks of range 1), (final width 0, final width 1)).  Waits
+        for the device (a synchronous copy); call after the decode has completed."""
+        import torch
+
+        if stream is None:
+            stream = torch.cuda.current_stream(torch.device("cuda", self._device))
+        ws = self._ws.get(int(stream.cuda_stream))
+        if ws is None:
+            raise ValueError("repack_stats: no decode_device has run on this stream")
+        out = (C.c_int32 * 4)()
+        check(_lib.load().qr_decode_repack_stats(self._h, int(ld), int(max_iterations), C.c_void_p(ws.data_ptr()),
+                                                 ws.numel(), out), "repack_stats")
+        return (int(out[0]), int(out[1])), (int(out[2]), int(out[3]))
+
     #: how many per-stream workspaces a Decoder keeps (each is E*ld*8 bytes of messages)
     max_workspaces = 2
 

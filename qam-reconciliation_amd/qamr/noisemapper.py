@@ -30,6 +30,28 @@ def _check_batch(B, ld, what):
         raise ValueError(f"{what}: need ld % 64 == 0 and 0 < B <= ld (B={B}, ld={ld})")
 
 
+def F_Z(z, mu, sigma):
+    """noisemapper.pyx:66-79: the Gaussian CDF 0.5 (1 + erf((z - mu) / (sqrt(2) sigma))) at every
+    z, with scipy's erf as the reference.  Off the hot path (a host helper)."""
+    from scipy.special import erf
+
+    z = np.asarray(z)
+    if z.dtype != np.float64:
+        raise ValueError(f"Buffer dtype mismatch, expected 'double' but got '{z.dtype}'")
+    z = np.ascontiguousarray(z.ravel())
+    return 0.5 * (1 + erf((z - float(mu)) / (math.sqrt(2) * float(sigma))))
+
+
+def view_dist_cut(x):
+    """noisemapper.pyx:82-98 (``__view_dist_cut``): every x clipped to the probability range,
+    0 below 0, 1 from 1 on (NaN stays NaN, as the reference's comparisons leave it)."""
+    x = np.asarray(x)
+    if x.dtype != np.float64:
+        raise ValueError(f"Buffer dtype mismatch, expected 'double' but got '{x.dtype}'")
+    x = np.ascontiguousarray(x.ravel())
+    return np.where(x < 0, 0.0, np.where(x >= 1, 1.0, x))
+
+
 def host_tables(a, th, p, sigma, bps):
     """The O(M^2) host tables of NoiseMapper.__cinit__ (noisemapper.pyx:166-235),
     with C erf/log semantics: (fwrd_transition_probability, back_transition_probability,

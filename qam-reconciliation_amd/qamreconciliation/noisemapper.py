@@ -5,9 +5,12 @@ variants (noisemapper.pyx:775-816: they override ``g``/``g_inv`` with a half-ord
 flip rule, while ``demap_lappr`` still follows ``sign_config``) are not on the
 reconciliation hot path and are out of scope: they import,
 so ``from qamreconciliation import *`` works, but constructing one raises."""
-from qamr.noisemapper import NoiseDemapper, NoiseMapper  # noqa: F401
+from qamr.noisemapper import F_Z, NoiseDemapper, NoiseMapper, view_dist_cut  # noqa: F401
 
-__all__ = ["NoiseMapper", "NoiseDemapper", "NoiseMapperFlipSign", "NoiseMapperAntiFlipSign"]
+# the reference's module-level cpdef (noisemapper.pyx:90); no name mangling at module level
+globals()["__view_dist_cut"] = view_dist_cut
+
+__all__ = ["NoiseMapper", "NoiseDemapper", "NoiseMapperFlipSign", "NoiseMapperAntiFlipSign", "F_Z"]
 
 
 class _OutOfScope(NoiseMapper):

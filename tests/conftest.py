@@ -58,7 +58,7 @@ def assert_llr_close(got, ref, rtol=LLR_RTOL, atol=LLR_ATOL):
 
 def assert_bit_exact(got, ref):
     """Identical doubles (signed zeros included); NaN matches NaN whatever its payload.
-    The decoder's default arithmetic (knob math = 0, glibc_math.hpp) reproduces the
+    The decoder's arithmetic (glibc_math.hpp, the only one) reproduces the
     reference's exp/log, so its outputs must equal the reference's bit for bit."""
     got = np.ascontiguousarray(got, np.float64)
     ref = np.ascontiguousarray(ref, np.float64)

@@ -345,9 +345,28 @@ def gen_noise_search():
     np.savez_compressed(os.path.join(HERE, "noise_search.npz"), **out)
 
 
+def gen_module_funcs():
+    """The module-level cpdefs of noisemapper.pyx: F_Z(z, mu, sigma) (:66-79) and
+    __view_dist_cut(x) (:82-98) on edge and random points."""
+    import qamreconciliation.noisemapper as nmod
+
+    rng = np.random.default_rng(77)
+    z = np.concatenate([np.array([0.0, -0.0, 1.0, -1.0, 1e-300, -1e300, 1e300, 40.0, -40.0, np.inf, -np.inf, np.nan]),
+                        rng.normal(0, 3, 40)])
+    out = {"z": z}
+    for c, (mu, sigma) in enumerate([(0.0, 1.0), (1.5, 0.3), (-2.0, 4.0), (0.0, 1e-3)]):
+        out[f"F_Z_{c}"] = np.asarray(nmod.F_Z(z.copy(), mu, sigma))
+        out[f"F_Z_{c}_args"] = np.array([mu, sigma])
+    x = np.concatenate([np.array([-1.0, -0.0, 0.0, 1e-300, 0.5, 1 - 2 ** -53, 1.0, 1.5, np.inf, -np.inf, np.nan]),
+                        rng.uniform(-0.5, 1.5, 30)])
+    out["x"] = x
+    out["dist_cut"] = np.asarray(getattr(nmod, "__view_dist_cut")(x.copy()))
+    np.savez_compressed(os.path.join(HERE, "module_funcs.npz"), **out)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["hamming", "node_rules", "reg1008", "demap", "pam16_nan", "llr_sources", "dvbs2",
-                             "dvbs2_16pam", "noise_search"]
+                             "dvbs2_16pam", "noise_search", "module_funcs"]
     for w in which:
         t = time.time()
         print(f"[golden] {w}", flush=True)

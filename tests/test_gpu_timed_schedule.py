@@ -121,13 +121,17 @@ def test_reference_frames_in_timed_batch(gpu, fname, key, bps, snr, B):
             assert_bit_exact(f[g[f"{key}_sample_idx"]], g[f"{key}_sample_final"])
 
 
-@pytest.mark.parametrize("bps,snr,B,mi", [(2, 4.0, 1024, 50), (4, 14.5, 1024, 50), (2, 3.8, 2048, 50),
-                                          (2, 4.0, 1000, 50), (2, 4.0, 1024, 22)])
+@pytest.mark.parametrize("bps,snr,B,mi", [(2, 4.0, 4096, 50), (4, 14.5, 4096, 50), (2, 4.0, 1024, 50),
+                                          (4, 14.5, 1024, 50), (2, 3.8, 2048, 50), (2, 4.0, 1000, 50),
+                                          (2, 4.0, 1024, 22)])
 def test_column_repack_vs_oracle(gpu, bps, snr, B, mi):
-    """Converging batches under the column repack (knob repack, default on: a range whose
-    running frames fill at most half its columns moves them to the front of a fresh column
-    set): every frame identical to the run without it, and the frames that ran longest --
-    the ones that went through the repacks -- bit-exact against the oracle."""
+    """Converging batches under the column repack (knob repack, default on: when a range's
+    running frames fill at most repack_pct = 75 % of its columns, the device moves them to the
+    front of the range), incl. the bench's own B = 4096 batches of its converging operating
+    points (BENCH op_dvbs2_4pam_4.0dB / op_dvbs2_16pam_14.5dB): every frame identical to the
+    runs with the narrow kernels off and with no repack at all, the frames that ran longest --
+    the ones that went through the repacks -- and frames spread over both ranges bit-exact
+    against the oracle, and the device did repack (reference: decoder.pyx:424-436)."""
     import torch
     from qamr import _lib
 
@@ -135,7 +139,7 @@ def test_column_repack_vs_oracle(gpu, bps, snr, B, mi):
     vid, cid, dec, pipe, b = _pipeline(bps, snr, B, seed=300 + int(10 * snr), max_iterations=mi)
     lappr = pipe.demap(b)
     saved = {k: _lib.tune_get(k) for k in ("repack", "narrow")}
-    outs = []
+    outs, stats = [], []
     try:
         # repacked ranges of <= 64 columns on the narrow (lane = (check, frame)) sweeps / on the
         # frame-parallel ones; then no repack at all
@@ -144,15 +148,19 @@ def test_column_repack_vs_oracle(gpu, bps, snr, B, mi):
             _lib.tune_set("narrow", nw)
             outs.append([x.clone() for x in pipe.decode(lappr, b)])
             torch.cuda.synchronize()
+            stats.append(dec.repack_stats(pipe.ld, mi))
     finally:
         for k, v in saved.items():
             _lib.tune_set(k, v)
+    (rep0, rep1), (w0, w1) = stats[0]
+    assert rep0 + rep1 > 0, stats[0]                  # the device repacked
+    assert min(w0, w1) < pipe.ld // 2, stats[0]
+    assert stats[2] == ((0, 0), (pipe.ld // 2, pipe.ld // 2))  # repack off: never
     f1, s1, i1 = outs[0]
     for f0, s0, i0 in outs[1:]:
         assert torch.equal(s1, s0) and torch.equal(i1, i0)
         assert torch.equal(f1[:, :B].view(torch.int64), f0[:, :B].view(torch.int64))
     its = i1.cpu().numpy()
-    assert its.max() - its.min() >= 4  # frames stop over many iterations: ranges get repacked
     cols = np.unique(np.r_[np.argsort(-its, kind="stable")[:8], _cols(B, 8)])
     ct = torch.as_tensor(cols, device=lappr.device)
     L = lappr[:, ct].T.contiguous().cpu().numpy()
@@ -160,3 +168,48 @@ def test_column_repack_vs_oracle(gpu, bps, snr, B, mi):
     s2, i2, fo = O.OracleCode(vid, cid).decode_batch(L, Sy, mi)
     assert np.array_equal(s1[ct].cpu().numpy(), s2) and np.array_equal(i1[ct].cpu().numpy(), i2)
     assert_bit_exact(f1[:, ct].T.contiguous().cpu().numpy(), fo)
+
+
+def test_repack_decode_is_asynchronous_and_capturable(gpu):
+    """qr_decode_batch_device keeps its contract with the column repack on (include/qamr.h):
+    on the bench's 4-PAM 4.0 dB B = 4096 batch the call returns while the GPU is still
+    decoding (the host never waits: every repack decision is taken on the device), and a
+    HIP-graph capture of the same decode replays bit-identically to the eager decode, the
+    device repacking inside the graph."""
+    import time
+
+    import torch
+
+    _assert_timed_defaults()
+    B, mi = 4096, 50
+    vid, cid, dec, pipe, b = _pipeline(2, 4.0, B, seed=340)
+    lappr = pipe.demap(b)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        dec.decode_device(lappr, b.synd, B, mi)  # warm-up: allocates this stream's workspace
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        t0 = time.perf_counter()
+        ref = dec.decode_device(lappr, b.synd, B, mi)
+        t_ret = time.perf_counter() - t0
+        end = torch.cuda.Event()
+        end.record(s)
+        pending = not end.query()
+    torch.cuda.synchronize()
+    t_all = time.perf_counter() - t0
+    eager_stats = dec.repack_stats(pipe.ld, mi, stream=s)
+    assert pending, (t_ret, t_all)
+    assert sum(eager_stats[0]) > 0, eager_stats
+    fin = torch.full_like(lappr, np.nan)
+    succ = torch.zeros(B, dtype=torch.uint8, device=lappr.device)
+    its = torch.zeros(B, dtype=torch.int32, device=lappr.device)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        dec.decode_device(lappr, b.synd, B, mi, fin, succ, its)
+    g.replay()
+    torch.cuda.synchronize()
+    graph_stats = dec.repack_stats(pipe.ld, mi, stream=s)
+    assert sum(graph_stats[0]) > 0, graph_stats
+    assert torch.equal(succ, ref[1]) and torch.equal(its, ref[2])
+    assert torch.equal(fin[:, :B].view(torch.int64), ref[0][:, :B].view(torch.int64))

@@ -5,7 +5,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import ROOT, golden
+from conftest import ROOT, assert_bit_exact, golden
 
 
 def test_alphabet_tables_vs_reference():
@@ -74,3 +74,18 @@ def test_count_errors_semantics():
     assert count_errors_from_lappr(l, w) == O.count_errors_from_lappr(l, w)
     with pytest.raises(ValueError):
         count_errors_from_lappr(l, w[:10])
+
+
+def test_noisemapper_module_functions_vs_reference():
+    """The module-level cpdefs F_Z (noisemapper.pyx:66-79) and __view_dist_cut (:82-98) of the
+    drop-in equal the reference's outputs bit for bit (tests/golden/module_funcs.npz, from the
+    reference built by oracle/Makefile ref)."""
+    import qamreconciliation.noisemapper as nmod
+
+    g = golden("module_funcs.npz")
+    for c in range(4):
+        mu, sigma = g[f"F_Z_{c}_args"]
+        assert_bit_exact(nmod.F_Z(g["z"], mu, sigma), g[f"F_Z_{c}"])
+    assert_bit_exact(getattr(nmod, "__view_dist_cut")(g["x"]), g["dist_cut"])
+    with pytest.raises(ValueError):
+        nmod.F_Z(g["z"].astype(np.float32), 0.0, 1.0)
