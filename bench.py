@@ -62,15 +62,20 @@ SIMDS, CLOCK_HZ = 1024, 2.4e9
 # (k_check<7> under the default schedule, k_fused<7> under split = 2) and the fused demap
 PRICED = ("check_d7", "fused_d7", "demap")
 
-# (name, workload, snr, batch, steps, BASELINE.json config it measures)
+# (name, workload, snr, batch, steps, BASELINE.json config it measures, launches timed with hipEvents
+#  inside its timed region, CPU leg)
 SECONDARY = [
-    ("configs1_reg1008_4pam", "reg1008_4pam", 3.0, 1024, 50, "configs[1]: reg-(3,6) N=1008, 4-PAM, B=1024"),
+    ("configs1_reg1008_4pam", "reg1008_4pam", 3.0, 1024, 50, "configs[1]: reg-(3,6) N=1008, 4-PAM, B=1024",
+     ("resident_d6", "iter_d6"), False),
     ("configs3_dvbs2_16pam", "dvbs2_16pam", 13.0, 4096, 3,
-     "configs[3]: N=64800 16-PAM, demap fused into the step, B=4096, 13 dB (all 50 iterations)"),
+     "configs[3]: N=64800 16-PAM, demap fused into the step, B=4096, 13 dB (all 50 iterations)",
+     ("check_d7", "demap"), True),
     ("op_dvbs2_4pam_4.0dB", "dvbs2_4pam", 4.0, 4096, 3,
-     "configs[2] code at its converging operating point 4.0 dB (frames stop early)"),
+     "configs[2] code at its converging operating point 4.0 dB (frames stop early)",
+     ("check_d7", "narrow_d7", "repack"), False),
     ("op_dvbs2_16pam_14.5dB", "dvbs2_16pam", 14.5, 4096, 3,
-     "configs[3] at its converging operating point 14.5 dB (demap fused)"),
+     "configs[3] at its converging operating point 14.5 dB (demap fused)",
+     ("check_d7", "narrow_d7", "repack", "demap"), False),
 ]
 
 
@@ -332,12 +337,15 @@ def kernel_clock(args):
         return None
 
 
-def kernel_stats():
+KERNEL_KEYS = ("check", "check_d7", "check_d6", "check1", "fused_d7", "var", "var_init", "parity", "status", "demap",
+               "iter_d6", "resident_d6", "narrow_d7", "repack")
+
+
+def kernel_stats(keys=KERNEL_KEYS):
     import qamr
 
     out = {}
-    for k in ("check", "check_d7", "check_d6", "check1", "fused_d7", "var", "var_init", "parity", "status", "demap",
-              "iter_d6", "resident_d6"):
+    for k in keys:
         ms, n = qamr.profile_query(k)
         if n:
             out[k] = {"avg_us": 1e3 * ms / n, "launches": n, "total_ms": ms}
@@ -429,16 +437,32 @@ def roofline(args, w, kstats, dev, world=1):
 
 def secondary(args, rank, local):
     """configs[1], configs[3] and the converging operating points, each on its own
-    resident batch, timed separately from the headline (same step definition)."""
+    resident batch, timed separately from the headline (same step definition).  Each carries
+    the hipEvent-timed average of its dominant launches (recorded on their launch streams inside
+    its timed region) so a kernel trace of the same config can be reconciled with its step; the
+    configs[3] line also carries its CPU baseline (demap + decode on the host cores, SURVEY.md
+    8(d)'s demap leg)."""
+    import types
+
+    import qamr
     import torch
 
     out = {}
-    for name, wl, snr, batch, steps, what in SECONDARY:
+    for name, wl, snr, batch, steps, what, keys, cpu_leg in SECONDARY:
         w = Work(wl, snr, batch, args.max_iter, args.alpha, args.seed, rank, local)
-        el = timed_region(w.step, w.sync, steps, 1, device=w.dev)
+
+        def before(keys=keys):
+            qamr.profile_reset()
+            qamr.profile_select(keys)
+            qamr.profile_enable(True)
+
+        el = timed_region(w.step, w.sync, steps, 1, before, lambda: qamr.profile_enable(False), device=w.dev)
         out[name] = {"frames_per_s": round(w.B * steps / el, 1), "ms_per_step": round(1e3 * el / steps, 3),
                      "steps": steps, "batch": w.B, "snr_db": w.snr, "mean_iterations": round(w.mean_iterations(), 3),
-                     "what": what}
+                     "what": what, "kernels": kernel_stats(keys)}
+        if cpu_leg and args.cpu_seconds > 0:
+            out[name]["cpu_baseline"] = cpu_baseline(types.SimpleNamespace(workload=wl, max_iter=args.max_iter), w,
+                                                     args.cpu_seconds)
         w.free()
         del w
         torch.cuda.empty_cache()
@@ -472,10 +496,12 @@ def cpu_baseline(args, w, budget_s):
         xs = w.batch.x[:, :nfr].cpu().numpy().T.copy()
     else:
         L = w.lappr[:, :nfr].cpu().numpy().T.copy()
-    frames, t0, rounds = 0, time.perf_counter(), 0
+    frames, t0, rounds, t_demap = 0, time.perf_counter(), 0, 0.0
     while True:
         if w.fused:
+            td = time.perf_counter()
             L = np.stack([nm.demap_lappr_array(nh[f], xs[f], nthreads=cores) * w.alpha for f in range(nfr)])
+            t_demap += time.perf_counter() - td
         code.decode_batch(L, synd, args.max_iter, nthreads=cores)
         frames += nfr
         rounds += 1
@@ -494,9 +520,16 @@ def cpu_baseline(args, w, budget_s):
     out = {"value": value, "unit": "frames/s", "cores": cores, "kind": "port",
            "sample": f"{frames} frames ({rounds} rounds x {nfr}) of the same workload in {el:.1f} s, "
                      f"oracle/qamr_oracle.c (gcc -O2 -ffp-contract=off, OpenMP over frames) on {cpu_model}"}
+    if w.fused:
+        out["demap_s_per_frame"] = t_demap / frames
+        out["decode_s_per_frame"] = (el - t_demap) / frames
+        out["note"] = ("one step = NoiseMapper.demap_lappr_array (16-PAM, noisemapper.pyx:544-559) + Decoder._decode "
+                       "per frame, frames in parallel over the cores; demap / decode split per frame of wall time")
     cal = cpu_calibration()
     if cal and args.workload in cal.get("workloads", {}):
         c = cal["workloads"][args.workload]
+        if w.fused:
+            out["demap_ratio_vs_cython"] = c.get("demap_ratio_port_over_cython")
         out["ratio_vs_cython"] = c["ratio_port_over_cython"]
         out["cython_equivalent_frames_per_s"] = value / c["ratio_port_over_cython"]
         out["calibration"] = (f"port/Cython speed ratio {c['ratio_port_over_cython']:.3f} measured on 1 core of the "
