@@ -72,10 +72,10 @@ SECONDARY = [
      ("check_d7", "demap"), True),
     ("op_dvbs2_4pam_4.0dB", "dvbs2_4pam", 4.0, 4096, 3,
      "configs[2] code at its converging operating point 4.0 dB (frames stop early)",
-     ("check_d7", "narrow_d7", "repack"), False),
+     ("check_d7", "repack"), False),
     ("op_dvbs2_16pam_14.5dB", "dvbs2_16pam", 14.5, 4096, 3,
      "configs[3] at its converging operating point 14.5 dB (demap fused)",
-     ("check_d7", "narrow_d7", "repack", "demap"), False),
+     ("check_d7", "repack", "demap"), False),
 ]
 
 
@@ -338,7 +338,7 @@ def kernel_clock(args):
 
 
 KERNEL_KEYS = ("check", "check_d7", "check_d6", "check1", "fused_d7", "var", "var_init", "parity", "status", "demap",
-               "iter_d6", "resident_d6", "narrow_d7", "repack")
+               "iter_d6", "resident_d6", "repack")
 
 
 def kernel_stats(keys=KERNEL_KEYS):

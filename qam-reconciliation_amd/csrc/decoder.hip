@@ -135,12 +135,10 @@ struct CheckArgs {
     int per_t;
     // Column repack (run_split2): sel -> the range's RangeSel, or null.  Once the device has
     // repacked the range (sel[kSelOn]) its posteriors and syndrome bits live in the work set
-    // (post_w, synd_w).  narrow: a narrow kernel is launched beside this one for the same range;
-    // the regular kernel then leaves when sel[kSelNarrow] is set, the narrow one when it is not.
+    // (post_w, synd_w).
     const int32_t *sel;
     const double *post_w;
     const uint8_t *synd_w;
-    int narrow;
 };
 
 // One variable sweep over the frame columns [f_off, f_off + ny*ft).
@@ -165,14 +163,13 @@ struct VarArgs {
     const int32_t *sel;  // as CheckArgs: the range's RangeSel or null; work-set LAPPRs / posteriors
     const double *lappr_w;
     double *post_w;
-    int narrow;
 };
 
 // The state of one frame range of the two-stream schedule, in device memory (the workspace's
 // count block), read by every launch of that range and written only by k_repack_commit: whether
 // the range has moved to the repack work set, its width there (its running frames occupy the
-// first columns), whether the narrow kernels sweep it, and how many repacks it went through.
-enum RangeSelField { kSelOn = 0, kSelW = 1, kSelNarrow = 2, kSelRepacks = 3, kSelInts = 4 };
+// first columns), and how many repacks it went through.
+enum RangeSelField { kSelOn = 0, kSelW = 1, kSelRepacks = 2, kSelInts = 4 };
 
 // Kernel-uniform: the arrays a range's launch reads once the device has repacked the range.
 __device__ __forceinline__ void select_range(CheckArgs &a) {
@@ -186,10 +183,6 @@ __device__ __forceinline__ void select_range(VarArgs &a) {
         a.lappr = a.lappr_w;
         a.post = a.post_w;
     }
-}
-// the regular sweep of a range the narrow kernels sweep (both are launched) leaves
-__device__ __forceinline__ bool swept_narrow(const int32_t *sel, int narrow) {
-    return narrow && sel && sld(sel + kSelNarrow);
 }
 
 // Active-frame compaction (converging operating points, decoder.pyx:431-433: frames stop
@@ -416,7 +409,6 @@ template <int D, int MODE, bool NT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) k_check(CheckArgs a) {
     __shared__ GlibcTablesBP tab;
     __shared__ double hb[kPackLdsDoubles];
-    if (swept_narrow(a.sel, a.narrow)) return;  // kernel-uniform
     select_range(a);
     unsigned bx = blockIdx.x, by = blockIdx.y;
     int per = a.g.per;
@@ -446,7 +438,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
 
 template <bool INIT, bool NT>
 __global__ void __launch_bounds__(256) k_var(VarArgs a) {
-    if (swept_narrow(a.sel, a.narrow)) return;  // kernel-uniform
     select_range(a);
     if (a.gs) {  // capped grid: tile t = (bx fastest, by), the grid's blocks sweep a moving window
         unsigned ny = a.nby, stride = gridDim.x;
@@ -473,76 +464,6 @@ __global__ void __launch_bounds__(256) k_var(VarArgs a) {
     var_block<INIT, NT>(a, blockIdx.x, blockIdx.y);
 }
 
-// ---------------------------------------------------------------------------------------
-// Narrow sweeps of a repacked range of at most 64 columns (the last running frames of a
-// converging batch).  The frame-parallel sweeps give every check a 64-lane wave of frames, so a
-// range with a handful of running frames still pays a whole wave per check; here a wave is 16
-// frames x 4 checks (lane = (check, frame), kNarrowFrames frames per group, one group per
-// blockIdx.y): the 16 frames of a group are consecutive columns, so each message row access is
-// one 128-byte line, and a group with no listed frame leaves at once.  The CSR is read per lane.
-// Each message is the same operation on the same operands as in check_block / var_block.
-constexpr int kNarrowFrames = 16;
-constexpr int kNarrowNodes = 256 / kNarrowFrames;  // checks (variables) per workgroup
-
-template <int D, bool FIN>
-__device__ __forceinline__ void check_narrow_block(const CheckArgs &a, const GlibcTablesBP &tab, double *hb) {
-    bool live;
-    const int p = (int)blockIdx.y * kNarrowFrames + (int)(threadIdx.x % kNarrowFrames);
-    const int f = lane_frame(a.alist, a.acount, a.f_off, p, live);
-    const bool act = live && a.active[f] != 0;
-    if (!wave_any(act)) return;  // wave-uniform: the packed update needs whole waves
-    const int64_t ci = (int64_t)blockIdx.x * kNarrowNodes + (int64_t)(threadIdx.x / kNarrowFrames);
-    const bool valid = ci < a.n_checks;
-    const int cc = a.checks[valid ? ci : a.n_checks - 1];
-    const int base = a.chk_ptr[cc];
-    const size_t ld = a.ld;
-    const uint8_t sb = a.synd[(size_t)cc * ld + f];
-    uint32_t par = sb;
-    double m[D];
-#pragma unroll
-    for (int i = 0; i < D; ++i) {
-        const double pv = a.post[(size_t)a.chk_var[base + i] * ld + f];
-        par ^= (pv < 0.0) ? 1u : 0u;                                  // decoder.pyx:243-246
-        m[i] = pv - a.c2v[(size_t)a.chk_edge[base + i] * ld + f];      // :296-297
-    }
-    double out[D];
-    check_strict_packed<D, FIN ? kClampFinite : kClampFull>(m, out, hb + (threadIdx.x >> 6) * kPackWaveDoubles, tab,
-                                                            GlibcK::pinned());
-    const double s = sb ? -1.0 : 1.0;
-    if (valid && act) {
-#pragma unroll
-        for (int i = 0; i < D; ++i) a.c2v[(size_t)a.chk_edge[base + i] * ld + f] = s * out[i];
-        if (par == 1u) a.unsat[f] = 1;  // benign race: every writer stores 1
-    }
-}
-
-template <int D>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) k_check_narrow(CheckArgs a) {
-    __shared__ GlibcTablesBP tab;
-    __shared__ double hb[4 * kPackWaveDoubles];
-    if (!sld(a.sel + kSelNarrow)) return;  // kernel-uniform: the regular kernel sweeps
-    select_range(a);
-    if (!frames_block_live(a.acount, blockIdx.y * kNarrowFrames, 0)) return;  // block-uniform
-    stage_glibc_tables(&tab, a.gglibc);
-    if (a.finite && sld(a.finite)) check_narrow_block<D, true>(a, tab, hb);
-    else check_narrow_block<D, false>(a, tab, hb);
-}
-
-__global__ void __launch_bounds__(256) k_var_narrow(VarArgs a) {
-    if (!sld(a.sel + kSelNarrow)) return;  // kernel-uniform: the regular kernel sweeps
-    select_range(a);
-    if (!frames_block_live(a.acount, blockIdx.y * kNarrowFrames, 0)) return;  // block-uniform
-    bool live;
-    const int p = (int)blockIdx.y * kNarrowFrames + (int)(threadIdx.x % kNarrowFrames);
-    const int f = lane_frame(a.alist, a.acount, a.f_off, p, live);
-    const int64_t v = (int64_t)blockIdx.x * kNarrowNodes + (int64_t)(threadIdx.x / kNarrowFrames);
-    if (!live || v >= a.V || !a.active[f]) return;
-    const size_t ld = a.ld;
-    double pv = a.lappr[(size_t)v * ld + f];
-    const int b = a.var_ptr[v], e = a.var_ptr[v + 1];
-    for (int k = b; k < e; ++k) pv += a.c2v[(size_t)a.var_edge[k] * ld + f];  // decoder.pyx:292-293
-    a.post[(size_t)v * ld + f] = pv;
-}
 
 // ---------------------------------------------------------------------------------------
 // Small codes (configs[1], reg-(3,6) N=1008): ONE launch per iteration.  A sweep of such a
@@ -672,7 +593,7 @@ constexpr int kResStaticLds = (int)sizeof(GlibcTablesBP) + (kResThreads / 64) * 
 struct ResArgs {
     int C, V, B, ld, max_it;
     const int32_t *chk_var;              // check CSR: check c's variables at D c .. D c + D - 1
-    const int32_t *var_ptr, *var_slot;   // per variable, its edges (ascending) as check-CSR slots
+    const int32_t *var_ptr, *var_msg;    // per variable, its edges (ascending) as LDS message indices
     const double *lappr;
     const uint8_t *synd;
     double *post;
@@ -749,14 +670,26 @@ __device__ __forceinline__ void resident_loop(const ResArgs &a, int f, double *m
             res_finish(a, f, post, 1, t - 1);
             return;
         }
-        for (int v = tid; v < a.V; v += kResThreads) {  // decoder.pyx:285-298
-            double p = a.lappr[(size_t)v * ld + f];
-            const int b = a.var_ptr[v], e = a.var_ptr[v + 1];
-            for (int k = b; k < e; ++k) {
-                const int sl = a.var_slot[k], c = sl / D;
-                p += msg[(sl - c * D) * a.C + c];
+        // decoder.pyx:285-298, two variables per lane at a time: their (latency-bound, L1/L2)
+        // LAPPR and index loads are issued together; each sum keeps its ascending edge order
+        for (int v0 = tid; v0 < a.V; v0 += 2 * kResThreads) {
+            const int v1 = v0 + kResThreads;
+            const bool two = v1 < a.V;
+            const int w1 = two ? v1 : v0;
+            double p0 = a.lappr[(size_t)v0 * ld + f];
+            double p1 = a.lappr[(size_t)w1 * ld + f];
+            const int b0 = a.var_ptr[v0], e0 = a.var_ptr[v0 + 1];
+            const int b1 = a.var_ptr[w1], e1 = a.var_ptr[w1 + 1];
+            const int n = max(e0 - b0, e1 - b1);
+            for (int q = 0; q < n; ++q) {
+                const bool h0 = b0 + q < e0, h1 = b1 + q < e1;
+                const double m0 = msg[a.var_msg[h0 ? b0 + q : 0]];  // (edge 0: an in-bounds dummy)
+                const double m1 = msg[a.var_msg[h1 ? b1 + q : 0]];
+                if (h0) p0 += m0;
+                if (h1) p1 += m1;
             }
-            post[v] = p;
+            post[v0] = p0;
+            if (two) post[v1] = p1;
         }
         __syncthreads();
     }
@@ -947,15 +880,13 @@ __global__ void k_status(int f0, int f1, int t, int final_call, int32_t final_it
 // through LDS, one store per running frame.  STATUS: the status update of sweep t
 // (k_status, never the final call) is applied first, frame by frame, by the same thread:
 // one launch instead of two between the check sweeps of the two-stream schedule.
-// sel / fid_w as k_status (a repacked range holds frames only in its first sel[kSelW] columns);
-// hcount (or null): a host-mapped copy of the count, which the host reads without waiting to
-// size the range's later launches (run_split2).
+// sel / fid_w as k_status (a repacked range holds frames only in its first sel[kSelW] columns).
 template <bool STATUS>
 __global__ void __launch_bounds__(1024) k_compact(int f0, int f1, uint8_t *__restrict__ active,
                                                   int32_t *__restrict__ list, int32_t *__restrict__ count, int t,
                                                   const uint8_t *__restrict__ unsat_t, uint8_t *__restrict__ success,
                                                   int32_t *__restrict__ iters, const int32_t *sel,
-                                                  const int32_t *__restrict__ fid_w, int32_t *hcount) {
+                                                  const int32_t *__restrict__ fid_w) {
     __shared__ int wsum[16];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int32_t *fid = range_fid(sel, fid_w);
@@ -983,10 +914,7 @@ __global__ void __launch_bounds__(1024) k_compact(int f0, int f1, uint8_t *__res
         base += tot;
         __syncthreads();  // wsum is rewritten by the next chunk
     }
-    if (threadIdx.x == 0) {
-        *count = base;
-        if (hcount) *(volatile int32_t *)hcount = base;
-    }
+    if (threadIdx.x == 0) *count = base;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1105,9 +1033,8 @@ __global__ void __launch_bounds__(kRepackThreads) k_repack_rows(RepackArgs r) {
     }
 }
 
-// One workgroup after k_repack_rows: frame ids, list, active flags and the RangeSel.  allow_narrow:
-// the host launches the narrow kernels beside the regular ones for this range from here on.
-__global__ void __launch_bounds__(1024) k_repack_commit(RepackArgs r, int allow_narrow) {
+// One workgroup after k_repack_rows: frame ids, list, active flags and the RangeSel.
+__global__ void __launch_bounds__(1024) k_repack_commit(RepackArgs r) {
     int cnt, w, w_new;
     const bool go = repack_go(r, cnt, w, w_new);
     const bool on = sld(r.sel + kSelOn) != 0;
@@ -1132,14 +1059,10 @@ __global__ void __launch_bounds__(1024) k_repack_commit(RepackArgs r, int allow_
             r.active[f0 + p] = 0;
         }
     }
-    if (threadIdx.x == 0) {
-        const int on2 = (go || on) ? 1 : 0, w2 = go ? w_new : w;
-        if (go) {
-            r.sel[kSelOn] = 1;
-            r.sel[kSelW] = w2;
-            r.sel[kSelRepacks] += 1;
-        }
-        r.sel[kSelNarrow] = (on2 && w2 <= 64 && allow_narrow) ? 1 : 0;
+    if (go && threadIdx.x == 0) {
+        r.sel[kSelOn] = 1;
+        r.sel[kSelW] = w_new;
+        r.sel[kSelRepacks] += 1;
     }
 }
 
@@ -1244,7 +1167,7 @@ struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3},
         lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024}, var_pace{28},
         check_tail{4}, fused_iter{1}, iter_streams{2}, var_boost{4}, resident{1}, repack{1},
-        repack_pct{75}, narrow{1};
+        repack_pct{75};
 };
 static Tuning g_tune;
 
@@ -1292,12 +1215,10 @@ struct Plan {
     bool compact = false;  // sweeps of the main loop read the active-frame lists
     int var_pace = 0;      // variable sweeps: workgroups per 128 frames (0 = one per tile)
     // run_split2 with the device-steered column repack: every launch of a range carries the
-    // range's RangeSel (steer), the narrow kernels are launched beside the regular ones (narrow),
-    // parity-only sweeps read the active-frame lists too (list_parity: the final sweep)
+    // range's RangeSel (steer); parity-only sweeps read the active-frame lists too (list_parity:
+    // the final sweep)
     bool steer = false;
-    bool narrow = false;
     bool list_parity = false;
-    int32_t *hcount = nullptr;     // host-mapped copy of the status launches' counts, or null
 
     const int32_t *count_of(int f0) const { return w.acount + (f0 == 0 ? 0 : 1); }
     const int32_t *sel_of(int f0) const { return steer ? w.rsel + (f0 == 0 ? 0 : kSelInts) : nullptr; }
@@ -1329,7 +1250,6 @@ struct Plan {
         a.sel = sel_of(f0);
         a.post_w = w.rs.post;
         a.synd_w = w.rs.synd;
-        a.narrow = 0;
         return a;
     }
     VarArgs var_args(int f0, int f1) const {
@@ -1356,7 +1276,6 @@ struct Plan {
         a.sel = sel_of(f0);
         a.lappr_w = w.rs.lappr;
         a.post_w = w.rs.post;
-        a.narrow = 0;
         return a;
     }
 };
@@ -1389,25 +1308,6 @@ static int launch_check_class(const Plan &P, const DegreeClass &cls, const doubl
         a.nmain = a.nbx * (grid.y - 1);
         a.per_t = a.g.per / tail;
         grid = dim3((unsigned)(a.nmain + nbx_t), 1);
-    }
-    // knob narrow (default 1): a range the device has repacked to <= 64 columns (strict packed
-    // degrees) is swept by the narrow kernel, launched beside the regular one; which of the two
-    // runs is read from the range's RangeSel on the device (run_split2)
-    if (MODE == kNormal && P.narrow && P.compact && a.sel && cls.degree >= 2 && cls.degree <= kPackMaxDeg) {
-        a.narrow = 1;
-        const dim3 gn((unsigned)((cls.n + kNarrowNodes - 1) / kNarrowNodes), (unsigned)(64 / kNarrowFrames));
-        ProfScope pn(profiling_on() ? "narrow_d" + std::to_string(cls.degree) : std::string(), P.s);
-#define QR_NARROW(DD)                                         \
-    case DD:                                                  \
-        k_check_narrow<DD><<<gn, 256, 0, P.s>>>(a);           \
-        break;
-        switch (cls.degree) {
-            QR_NARROW(2) QR_NARROW(3) QR_NARROW(4) QR_NARROW(5) QR_NARROW(6) QR_NARROW(7) QR_NARROW(8) QR_NARROW(9)
-            QR_NARROW(10)
-            default: break;
-        }
-#undef QR_NARROW
-        QR_LAUNCH_CHECK();
     }
     ProfScope ps(profiling_on() ? std::string(MODE == kParityOnly ? "parity_d" : MODE == kFirst ? "check1_d" : "check_d") +
                                       std::to_string(cls.degree)
@@ -1452,12 +1352,6 @@ static int launch_var(const Plan &P, int f0, int f1, int32_t *finite = nullptr, 
     if (P.compact && !INIT) {
         a.alist = P.w.alist;
         a.acount = P.count_of(f0);
-    }
-    if (!INIT && P.narrow && P.compact && a.sel) {  // beside the regular sweep (knob narrow, as the checks)
-        a.narrow = 1;
-        const dim3 gn((unsigned)((P.code->V + kNarrowNodes - 1) / kNarrowNodes), (unsigned)(64 / kNarrowFrames));
-        k_var_narrow<<<gn, 256, 0, P.s>>>(a);
-        QR_LAUNCH_CHECK();
     }
     dim3 grid(a.nbx, a.nby);
     // Paced sweep (the two-stream schedule's variable sweeps, Plan::var_pace): at most var_pace
@@ -1527,7 +1421,7 @@ static int launch_status(const Plan &P, int f0, int f1, int t, int final_call, i
 static int launch_compact(const Plan &P, int f0, int f1) {
     if (!P.compact) return QR_OK;
     k_compact<false><<<1, 1024, 0, P.s>>>(f0, f1, P.w.active, P.w.alist, const_cast<int32_t *>(P.count_of(f0)), 0,
-                                          nullptr, nullptr, nullptr, P.sel_of(f0), P.w.rs.fid, nullptr);
+                                          nullptr, nullptr, nullptr, P.sel_of(f0), P.w.rs.fid);
     QR_LAUNCH_CHECK();
     return QR_OK;
 }
@@ -1538,8 +1432,7 @@ static int launch_status_compact(const Plan &P, int f0, int f1, int t, const uin
     if (!P.compact) return launch_status(P, f0, f1, t, 0, 0, unsat_t);
     ProfScope ps("status", P.s);
     k_compact<true><<<1, 1024, 0, P.s>>>(f0, f1, P.w.active, P.w.alist, const_cast<int32_t *>(P.count_of(f0)), t,
-                                         unsat_t, P.success, P.iters, P.sel_of(f0), P.w.rs.fid,
-                                         P.hcount ? P.hcount + (f0 == 0 ? 0 : 1) : nullptr);
+                                         unsat_t, P.success, P.iters, P.sel_of(f0), P.w.rs.fid);
     QR_LAUNCH_CHECK();
     return QR_OK;
 }
@@ -1636,29 +1529,10 @@ static int side_stream(const qr_code *code, hipStream_t *out) {
     return QR_OK;
 }
 
-// Host-mapped counts of the column repack (caller holds code->mu).  A decode still finishing on
-// another stream may write its counts while the next one starts: every decode takes the next of
-// kRepackSlots count pairs.
-constexpr int kRepackSlots = 32;
-static int repack_counts(const qr_code *code) {
-    if (!code->hc) {
-        void *hp = nullptr, *dp = nullptr;
-        hipError_t e = hipHostMalloc(&hp, 2 * kRepackSlots * sizeof(int32_t), hipHostMallocMapped);
-        if (e == hipSuccess) e = hipHostGetDevicePointer(&dp, hp, 0);
-        if (e != hipSuccess) {
-            if (hp) (void)hipHostFree(hp);
-            return set_error(QR_EDEVICE, "decode: host-mapped counts: %s", hipGetErrorString(e));
-        }
-        code->hc = (int32_t *)hp;
-        code->hc_dev = (int32_t *)dp;
-    }
-    return QR_OK;
-}
-
 // A repack decision point of the range starting at column f0 (full width h), on P.s: the device
 // decides and, when it repacks, moves the columns (k_repack_rows) and updates the range's state
 // (k_repack_commit).
-static int launch_repack(const Plan &P, int f0, int h, int allow_narrow) {
+static int launch_repack(const Plan &P, int f0, int h) {
     const qr_code *code = P.code;
     RepackArgs r;
     r.f0 = f0;
@@ -1682,9 +1556,11 @@ static int launch_repack(const Plan &P, int f0, int h, int allow_narrow) {
     r.fid_w = P.w.rs.fid;
     const int64_t rows = code->E + 2 * code->V + code->C;
     ProfScope ps("repack", P.s);
-    k_repack_rows<<<(unsigned)std::min<int64_t>(rows, 4096), kRepackThreads, 0, P.s>>>(r);
+    // 1 024 workgroups (4 per CU) walk the rows; when the device decides not to repack they all
+    // leave at once (a few microseconds on the variable stream)
+    k_repack_rows<<<(unsigned)std::min<int64_t>(rows, 1024), kRepackThreads, 0, P.s>>>(r);
     QR_LAUNCH_CHECK();
-    k_repack_commit<<<1, 1024, 0, P.s>>>(r, allow_narrow);
+    k_repack_commit<<<1, 1024, 0, P.s>>>(r);
     QR_LAUNCH_CHECK();
     return QR_OK;
 }
@@ -1701,51 +1577,19 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
     hipEvent_t fork = code->ev[0], cA = code->ev[1], cB = code->ev[2], vA = code->ev[3], vB = code->ev[4];
     const int ld = P.ld, h = ld / 2;  // ld % 512 == 0: both ranges are h columns wide
     // Column repack (knob repack, default 1; needs the workspace's work set), decided on the device
-    // (k_repack_rows / k_repack_commit at every decision point).  The host only picks launch
-    // shapes, from the host-mapped counts it reads WITHOUT waiting (each is an upper bound of
-    // every later count of its range, since counts only fall): while no frame of a range has
-    // stopped it skips that range's decision launches (no cost at 3 dB), it sizes the sweeps'
-    // grids to the count, leaves a sparse range's variable sweep unpaced, and once the count is at
-    // most 64 launches the narrow kernels beside the regular ones and lets the device switch to
-    // them.  Under stream capture nothing can be read: every decision point is launched, grids keep
-    // the full width and the narrow kernels stay off -- the same results, a slower tail.
-    // MI355X, round 4 (host-decided repack, copies on the variable stream): 4-PAM 4.0 dB +5.7 %,
-    // 16-PAM 14.5 dB +2.5 %; threshold (knob repack_pct) 75 % best of 65 / 75 / 85.
+    // at every decision point (k_repack_rows / k_repack_commit before each variable sweep of a
+    // range): the host enqueues the same launches whatever the data, never reads anything back
+    // and never waits, so the decode is asynchronous and capturable (the host runs far ahead of
+    // the GPU anyway: counts it could read without waiting would be an iteration-old at best).
     const bool rp = P.compact && P.w.repack && g_tune.repack.load();
-    bool capturing = false;
-    {
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        if (hipStreamIsCapturing(P.s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) capturing = true;
-    }
-    const bool hints = rp && !capturing;
-    if (hints) {
-        if (int rc0 = repack_counts(code)) return rc0;
-    }
     Plan base = P;
     base.steer = rp;
     Plan Pb = base;  // status launches (P.s)
-    const int32_t *hc = nullptr;
-    if (hints) {
-        const int slot = 2 * (int)(code->hc_gen++ % kRepackSlots);
-        code->hc[slot] = code->hc[slot + 1] = ld;
-        hc = code->hc + slot;
-        Pb.hcount = code->hc_dev + slot;
-    }
-    auto stale = [&](int k) -> int { return hints ? *(volatile const int32_t *)(hc + k) : ld; };
-    const int pct = std::clamp(g_tune.repack_pct.load(), 1, 90);
-    // the grid width of range k's sweeps: covers every frame its list can still hold
-    auto cols = [&](int k) -> int { return hints ? std::clamp((stale(k) + 63) / 64 * 64, 64, h) : h; };
-    bool steering[2] = {false, false}, narrow_on[2] = {false, false};
     Plan V = base;
     V.s = s2;
     V.var_pace = g_tune.var_pace.load();
     Plan C = base;
     C.lds_pad = std::max(0, g_tune.lds_pad_kb.load()) * 1024;
-    auto plan_for = [&](const Plan &Q, int k) {
-        Plan X = Q;
-        X.narrow = narrow_on[k];
-        return X;
-    };
     auto row = [&](int t) { return P.w.unsat + (size_t)t * ld; };
     // Knob side (default 1): the check sweeps of the small degree classes (DVB-S2: the one
     // degree-6 check) run on the variable stream right after the variable sweep they follow,
@@ -1760,17 +1604,15 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
         if (k != big) side_edges += code->classes[k].n * code->classes[k].degree;
     const bool side = g_tune.side.load() && code->classes.size() > 1 && side_edges * 8 <= code->E;
     auto checks_main = [&](int t, int k) {  // check sweep t >= 2 of range k on the check stream
-        const Plan Q = plan_for(C, k);
-        const int f0 = k * h, f1 = f0 + cols(k);
-        if (!side) return launch_checks<kNormal>(Q, P.post, row(t - 1), f0, f1);
+        const int f0 = k * h, f1 = f0 + h;
+        if (!side) return launch_checks<kNormal>(C, P.post, row(t - 1), f0, f1);
         const DegreeClass &cls = code->classes[big];
-        return P.nt ? launch_check_class<kNormal, true>(Q, cls, P.post, row(t - 1), f0, f1)
-                    : launch_check_class<kNormal, false>(Q, cls, P.post, row(t - 1), f0, f1);
+        return P.nt ? launch_check_class<kNormal, true>(C, cls, P.post, row(t - 1), f0, f1)
+                    : launch_check_class<kNormal, false>(C, cls, P.post, row(t - 1), f0, f1);
     };
     auto checks_side = [&](int t, int k) {  // the other classes of check sweep t, on V.s
         if (!side) return (int)QR_OK;
-        const Plan Q = plan_for(V, k);
-        return launch_checks<kNormal>(Q, P.post, row(t - 1), k * h, k * h + cols(k), big);
+        return launch_checks<kNormal>(V, P.post, row(t - 1), k * h, (k + 1) * h, big);
     };
     // range k's variable sweep, preceded by its repack decision point (the status launch it waits
     // for wrote the count the device decides on); the copies run under the other range's check
@@ -1778,18 +1620,9 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
     auto var_sweep = [&](int k) {
         const int f0 = k * h;
         if (rp) {
-            const int sc = stale(k);
-            if (capturing || steering[k] || sc < h) {
-                steering[k] = true;
-                if (hints && sc <= 64 && g_tune.narrow.load()) narrow_on[k] = true;
-                if (int rc0 = launch_repack(V, f0, h, narrow_on[k] ? 1 : 0)) return rc0;
-            }
+            if (int rc0 = launch_repack(V, f0, h)) return rc0;
         }
-        Plan Q = plan_for(V, k);
-        // the pacing spreads a full range's variable sweep over a full range's check launch; a
-        // sparse range's check launch is short, and so must be its variable sweep
-        if (hints && (int64_t)stale(k) * 100 <= (int64_t)h * pct) Q.var_pace = 0;
-        return launch_var<false>(Q, f0, f0 + cols(k));
+        return launch_var<false>(V, f0, f0 + h);
     };
     auto status = [&](int k, int ts) -> int {
         return launch_status_compact(Pb, k * h, (k + 1) * h, ts, row(ts));
@@ -1800,11 +1633,6 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
     if ((rc = launch_checks<kFirst>(C, P.post, row(0), 0, h))) return rc;
     QR_HIP(hipEventRecord(cA, P.s));
     for (int t = 1; t <= max_it; ++t) {
-        // every frame of both ranges has stopped (the counts the host sees lag, but only fall):
-        // the remaining iterations would sweep nothing -- leave the loop with both ranges at a
-        // status boundary (B after S_B(t-1), A after S_A(t-1)); the final parity check and
-        // status below then find no running frame
-        if (hints && t >= 3 && stale(0) == 0 && stale(1) == 0) break;
         QR_HIP(hipStreamWaitEvent(V.s, cA, 0));
         if ((rc = var_sweep(0))) return rc;
         if (t < max_it && (rc = checks_side(t + 1, 0))) return rc;
@@ -1840,7 +1668,7 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
     F.list_parity = true;
     for (int k = 0; k < 2; ++k) {
         const int f0 = k * h;
-        if ((rc = launch_checks<kParityOnly>(F, P.post, unsat_last, f0, f0 + cols(k)))) return rc;
+        if ((rc = launch_checks<kParityOnly>(F, P.post, unsat_last, f0, f0 + h))) return rc;
         if ((rc = launch_status(F, f0, f0 + h, max_it, 1, max_it, unsat_last))) return rc;
         ProfScope ps("repack", P.s);
         k_repack_output<<<dim3((unsigned)(h + 255) / 256, (unsigned)std::min<int64_t>(code->V, 2048)), 256, 0, P.s>>>(
@@ -1946,7 +1774,7 @@ static int run_resident(const qr_code *code, int B, int ld, const double *lappr,
     a.max_it = max_it;
     a.chk_var = code->d_chk_var;
     a.var_ptr = code->d_var_ptr;
-    a.var_slot = code->d_var_slot;
+    a.var_msg = code->d_var_msg;
     a.lappr = lappr;
     a.synd = synd;
     a.post = final_post;
@@ -2122,11 +1950,10 @@ static int free_code(qr_code *c) {
     (void)hipFree(c->d_chk_var);
     (void)hipFree(c->d_var_ptr);
     (void)hipFree(c->d_var_edge);
-    (void)hipFree(c->d_var_slot);
+    (void)hipFree(c->d_var_msg);
     (void)hipFree(c->d_gtab);
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
-    if (c->hc) (void)hipHostFree(c->hc);
     if (c->s2) (void)hipStreamDestroy(c->s2);
     delete c;
     return QR_OK;
@@ -2183,10 +2010,14 @@ int qr_code_create(const int64_t *e_to_v, const int64_t *e_to_c, int64_t nv, int
         return rc;
     }
     {
-        std::vector<int32_t> slot_of_edge((size_t)E), var_slot((size_t)E);
-        for (int64_t s = 0; s < E; ++s) slot_of_edge[(size_t)chk_edge[(size_t)s]] = (int32_t)s;
-        for (int64_t k = 0; k < E; ++k) var_slot[(size_t)k] = slot_of_edge[(size_t)var_edge[(size_t)k]];
-        if ((rc = upload(&code->d_var_slot, var_slot))) {
+        // the frame-resident decode's LDS message index of every edge, in the variable CSR's
+        // order: edge i of check c (check-CSR slot chk_ptr[c] + i) lives at i * C + c
+        std::vector<int32_t> msg_of_edge((size_t)E), var_msg((size_t)E);
+        for (int64_t c = 0; c < C; ++c)
+            for (int32_t s = chk_ptr[(size_t)c]; s < chk_ptr[(size_t)c + 1]; ++s)
+                msg_of_edge[(size_t)chk_edge[(size_t)s]] = (int32_t)((s - chk_ptr[(size_t)c]) * C + c);
+        for (int64_t k = 0; k < E; ++k) var_msg[(size_t)k] = msg_of_edge[(size_t)var_edge[(size_t)k]];
+        if ((rc = upload(&code->d_var_msg, var_msg))) {
             free_code(code);
             return rc;
         }
@@ -2249,7 +2080,7 @@ static std::atomic<int> *tune_knob(const char *name) {
         {"var_pace", &g_tune.var_pace},     {"check_tail", &g_tune.check_tail}, {"var_boost", &g_tune.var_boost},
         {"fused_iter", &g_tune.fused_iter}, {"iter_streams", &g_tune.iter_streams},
         {"resident", &g_tune.resident},   {"repack", &g_tune.repack},
-        {"repack_pct", &g_tune.repack_pct}, {"narrow", &g_tune.narrow},
+        {"repack_pct", &g_tune.repack_pct},
     };
     const std::string n = name ? name : "";
     for (const auto &k : knobs)

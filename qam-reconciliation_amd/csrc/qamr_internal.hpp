@@ -98,9 +98,9 @@ struct qr_code {
     // per variable, edge ids ascending.
     int32_t *d_chk_ptr = nullptr, *d_chk_edge = nullptr, *d_chk_var = nullptr;
     int32_t *d_var_ptr = nullptr, *d_var_edge = nullptr;
-    // per variable, edges ascending as above, each given by its position in the check CSR
-    // (chk_ptr[c] + i): the frame-resident small-code decoder's message index
-    int32_t *d_var_slot = nullptr;
+    // per variable, edges ascending as above, each given by the frame-resident small-code
+    // decoder's LDS message index i * C + c (edge i of check c)
+    int32_t *d_var_msg = nullptr;
     std::vector<DegreeClass> classes;
     int64_t fb_rows = 0;  // rows of the F scratch (sum over runtime-degree classes)
     qr::GlibcTables *d_gtab = nullptr; // strict box-plus: glibc exp/log data (glibc_math.hpp)
@@ -111,12 +111,6 @@ struct qr_code {
     mutable std::mutex mu;
     mutable hipStream_t s2 = nullptr;
     mutable hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-    // column repack of the two-stream schedule: host-mapped copies of the two ranges' running-
-    // frame counts (created on first use).  The host only ever reads them without waiting, as
-    // upper bounds of the counts still to come (counts only fall), to size launches; every
-    // decision that changes a result is taken on the device.
-    mutable int32_t *hc = nullptr, *hc_dev = nullptr;  // kRepackSlots pairs, one per decode in turn
-    mutable unsigned hc_gen = 0;
 };
 
 struct qr_demap {

@@ -129,7 +129,7 @@ def test_column_repack_vs_oracle(gpu, bps, snr, B, mi):
     running frames fill at most repack_pct = 75 % of its columns, the device moves them to the
     front of the range), incl. the bench's own B = 4096 batches of its converging operating
     points (BENCH op_dvbs2_4pam_4.0dB / op_dvbs2_16pam_14.5dB): every frame identical to the
-    runs with the narrow kernels off and with no repack at all, the frames that ran longest --
+    run with no repack at all, the frames that ran longest --
     the ones that went through the repacks -- and frames spread over both ranges bit-exact
     against the oracle, and the device did repack (reference: decoder.pyx:424-436)."""
     import torch
@@ -138,24 +138,20 @@ def test_column_repack_vs_oracle(gpu, bps, snr, B, mi):
     _assert_timed_defaults()
     vid, cid, dec, pipe, b = _pipeline(bps, snr, B, seed=300 + int(10 * snr), max_iterations=mi)
     lappr = pipe.demap(b)
-    saved = {k: _lib.tune_get(k) for k in ("repack", "narrow")}
+    saved = _lib.tune_get("repack")
     outs, stats = [], []
     try:
-        # repacked ranges of <= 64 columns on the narrow (lane = (check, frame)) sweeps / on the
-        # frame-parallel ones; then no repack at all
-        for rp, nw in ((1, 1), (1, 0), (0, 1)):
+        for rp in (1, 0):
             _lib.tune_set("repack", rp)
-            _lib.tune_set("narrow", nw)
             outs.append([x.clone() for x in pipe.decode(lappr, b)])
             torch.cuda.synchronize()
             stats.append(dec.repack_stats(pipe.ld, mi))
     finally:
-        for k, v in saved.items():
-            _lib.tune_set(k, v)
+        _lib.tune_set("repack", saved)
     (rep0, rep1), (w0, w1) = stats[0]
     assert rep0 + rep1 > 0, stats[0]                  # the device repacked
     assert min(w0, w1) < pipe.ld // 2, stats[0]
-    assert stats[2] == ((0, 0), (pipe.ld // 2, pipe.ld // 2))  # repack off: never
+    assert stats[1] == ((0, 0), (pipe.ld // 2, pipe.ld // 2))  # repack off: never
     f1, s1, i1 = outs[0]
     for f0, s0, i0 in outs[1:]:
         assert torch.equal(s1, s0) and torch.equal(i1, i0)
