@@ -942,9 +942,17 @@ __global__ void __launch_bounds__(1024) k_compact(int f0, int f1, uint8_t *__res
 // In-place compaction of a row (list ascending, so a column is only ever moved to a column at or
 // before it): chunks of columns in ascending order, all reads of a chunk complete before any of
 // its writes (one barrier); a later chunk reads only columns beyond every column written before.
+// The decision points run on the variable stream beside the other range's check launch, whose
+// waves hold 4 x 120 of the 512 VGPRs of a SIMD: the repack waves must fit in the 32 left, or
+// their workgroups are dispatched only as check workgroups retire (a first 48-VGPR version waited
+// ~0.26 ms per decision point at 4-PAM 4.0 dB).  So each workgroup owns whole rows, takes its
+// chunk's source columns from the list once (kRepackPer per thread, in registers for all of its
+// rows) and moves two rows per barrier: 2 x kRepackPer loads in flight per thread, the row base in
+// scalar registers and the column as a 32-bit offset.
 constexpr int kRepackThreads = 256;
-constexpr int kRepackPer = 8;  // columns per thread per chunk
+constexpr int kRepackPer = 4;  // columns per thread per chunk
 constexpr int kRepackChunk = kRepackThreads * kRepackPer;
+constexpr int kRepackGrid = 512;  // workgroups of k_repack_rows (2 per CU)
 
 struct RepackArgs {
     int f0, h, ld, pct;  // the range's first column and full width; repack threshold (percent)
@@ -979,68 +987,107 @@ __device__ __forceinline__ void loads_done_barrier() {
     __syncthreads();
 }
 
+// Raw buffer access to one row of a frame-innermost array (row base in scalar registers, the lane's
+// byte offset in a VGPR): an offset past the row reads 0 and drops the store, so slots past the
+// count need no branch.
 template <typename T>
-__device__ __forceinline__ void compact_row(const T *src, T *dst, const int32_t *list, int f0, int cnt) {
-    for (int p0 = 0; p0 < cnt; p0 += kRepackChunk) {
-        T v[kRepackPer];
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc_of(const T *rowp, int ld) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(rowp), (short)0, ld * (int)sizeof(T), 0x00020000);
+}
+__device__ __forceinline__ double rb_load(__amdgpu_buffer_rsrc_t r, uint32_t off, double) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+__device__ __forceinline__ uint8_t rb_load(__amdgpu_buffer_rsrc_t r, uint32_t off, uint8_t) {
+    return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+}
+__device__ __forceinline__ void rb_store(__amdgpu_buffer_rsrc_t r, uint32_t off, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(qr_u32x2, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void rb_store(__amdgpu_buffer_rsrc_t r, uint32_t off, uint8_t v) {
+    __builtin_amdgcn_raw_buffer_store_b8(v, r, off, 0, 0);
+}
+
+// One chunk of this workgroup's rows r = blockIdx.x + k gridDim.x < nrows of one array: element
+// (row, dcol0 + u * 256 + tid) <- (row, col[u]) for the slots with bit u of has, two rows per
+// barrier.
+template <typename T>
+__device__ __forceinline__ void compact_rows(const T *src, T *dst, int64_t nrows, int ld, int dcol0,
+                                             const uint32_t (&col)[kRepackPer], uint32_t has) {
+    constexpr uint32_t kNone = 0xFFFFFFF0u;  // past any row: loads 0, stores nothing
+    // col[u] already holds the byte offset of the source column, or kNone (see k_repack_rows)
+    const uint32_t dbase = (uint32_t)(dcol0 + (int)threadIdx.x) * (uint32_t)sizeof(T);
+    const int64_t G = gridDim.x;
+    for (int64_t r0 = blockIdx.x; r0 < nrows; r0 += 2 * G) {
+        const int64_t r1 = r0 + G;
+        const bool two = r1 < nrows;  // block-uniform
+        const auto s0 = row_rsrc_of(src + (size_t)r0 * ld, ld);
+        const auto s1 = row_rsrc_of(src + (size_t)(two ? r1 : r0) * ld, ld);
+        T v0[kRepackPer], v1[kRepackPer];
 #pragma unroll
         for (int u = 0; u < kRepackPer; ++u) {
-            const int p = p0 + u * kRepackThreads + (int)threadIdx.x;
-            v[u] = p < cnt ? src[list[f0 + p]] : T(0);
+            const uint32_t so = col[u] == kNone ? kNone : col[u] / (8u / (uint32_t)sizeof(T));
+            v0[u] = rb_load(s0, so, T(0));
+            v1[u] = rb_load(s1, so, T(0));
         }
         loads_done_barrier();
+        const auto d0 = row_rsrc_of(dst + (size_t)r0 * ld, ld);
+        const auto d1 = row_rsrc_of(dst + (size_t)(two ? r1 : r0) * ld, ld);
 #pragma unroll
         for (int u = 0; u < kRepackPer; ++u) {
-            const int p = p0 + u * kRepackThreads + (int)threadIdx.x;
-            if (p < cnt) dst[f0 + p] = v[u];
+            const uint32_t dof = ((has >> u) & 1u) ? dbase + (uint32_t)(u * kRepackThreads * sizeof(T)) : kNone;
+            rb_store(d0, dof, v0[u]);
+            if (two) rb_store(d1, dof, v1[u]);
         }
     }
 }
 
-// Grid-stride over the rows: [0, E) messages, [E, E + V) posteriors, [E + V, E + 2V) LAPPRs,
-// [E + 2V, E + 2V + C) syndrome bytes.
+// The row moves of a repack: messages in place, posteriors / LAPPRs / syndrome bytes from the
+// caller's arrays (first repack) or in place in the work set; each array's rows are owned by
+// workgroup (row mod gridDim.x) through every chunk, so a row's chunks run in ascending order.
 __global__ void __launch_bounds__(kRepackThreads) k_repack_rows(RepackArgs r) {
     int cnt, w, w_new;
     if (!repack_go(r, cnt, w, w_new)) return;  // kernel-uniform
     const bool on = sld(r.sel + kSelOn) != 0;
     const size_t ld = r.ld;
-    const int64_t rows = r.E + 2 * r.V + r.C;
-    for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
-        if (row < r.E) {
-            double *q = r.c2v + (size_t)row * ld;
-            compact_row<double>(q, q, r.list, r.f0, cnt);
-        } else if (row < r.E + r.V) {
-            const int64_t v = row - r.E;
-            double *dst = r.post_w + (size_t)v * ld;
-            if (on) {
-                // frames stopped since the last repack: their posteriors to the output first
-                // (read before the compaction's barrier, which orders them before its writes)
-                for (int q = threadIdx.x; q < w; q += kRepackThreads) {
-                    const int id = r.fid_w[r.f0 + q];
-                    if (id >= 0 && !r.active[r.f0 + q]) r.out_post[(size_t)v * ld + id] = dst[r.f0 + q];
-                }
+    const int f0 = r.f0;
+    if (on) {  // frames stopped since the last repack hand their posteriors to the output first
+        for (int64_t v = blockIdx.x; v < r.V; v += gridDim.x) {
+            const double *src = r.post_w + (size_t)v * ld + f0;
+            for (int q = threadIdx.x; q < w; q += kRepackThreads) {
+                const int id = r.fid_w[f0 + q];
+                if (id >= 0 && !r.active[f0 + q]) r.out_post[(size_t)v * ld + id] = src[q];
             }
-            compact_row<double>(on ? dst : r.out_post + (size_t)v * ld, dst, r.list, r.f0, cnt);
-        } else if (row < r.E + 2 * r.V) {
-            const int64_t v = row - r.E - r.V;
-            double *dst = r.lappr_w + (size_t)v * ld;
-            compact_row<double>(on ? dst : r.lappr_in + (size_t)v * ld, dst, r.list, r.f0, cnt);
-        } else {
-            const int64_t c = row - r.E - 2 * r.V;
-            uint8_t *dst = r.synd_w + (size_t)c * ld;
-            compact_row<uint8_t>(on ? dst : r.synd_in + (size_t)c * ld, dst, r.list, r.f0, cnt);
         }
+        loads_done_barrier();  // (every such read before any compaction write below)
+    }
+    for (int p0 = 0; p0 < cnt; p0 += kRepackChunk) {
+        // the chunk's source columns as byte offsets of a double row (a byte row divides by 8),
+        // kNone past the count
+        uint32_t col[kRepackPer], has = 0;
+#pragma unroll
+        for (int u = 0; u < kRepackPer; ++u) {
+            const int p = p0 + u * kRepackThreads + (int)threadIdx.x;
+            col[u] = p < cnt ? (uint32_t)r.list[f0 + p] * 8u : 0xFFFFFFF0u;
+            has |= (p < cnt ? 1u : 0u) << u;
+        }
+        const int dcol0 = f0 + p0;
+        compact_rows<double>(r.c2v, r.c2v, r.E, r.ld, dcol0, col, has);
+        compact_rows<double>(on ? r.post_w : r.out_post, r.post_w, r.V, r.ld, dcol0, col, has);
+        compact_rows<double>(on ? r.lappr_w : r.lappr_in, r.lappr_w, r.V, r.ld, dcol0, col, has);
+        compact_rows<uint8_t>(on ? r.synd_w : r.synd_in, r.synd_w, r.C, r.ld, dcol0, col, has);
     }
 }
 
-// One workgroup after k_repack_rows: frame ids, list, active flags and the RangeSel.
-__global__ void __launch_bounds__(1024) k_repack_commit(RepackArgs r) {
+// One workgroup (4 waves, one per SIMD) after k_repack_rows: frame ids, list, active flags and the
+// RangeSel.
+constexpr int kCommitThreads = 256;
+__global__ void __launch_bounds__(kCommitThreads) k_repack_commit(RepackArgs r) {
     int cnt, w, w_new;
     const bool go = repack_go(r, cnt, w, w_new);
     const bool on = sld(r.sel + kSelOn) != 0;
     if (go) {
         const int f0 = r.f0;
-        for (int p0 = 0; p0 < cnt; p0 += 1024) {
+        for (int p0 = 0; p0 < cnt; p0 += kCommitThreads) {
             const int p = p0 + (int)threadIdx.x;
             int id = 0;
             if (p < cnt) {
@@ -1054,7 +1101,7 @@ __global__ void __launch_bounds__(1024) k_repack_commit(RepackArgs r) {
                 r.active[f0 + p] = 1;
             }
         }
-        for (int p = cnt + (int)threadIdx.x; p < w; p += 1024) {
+        for (int p = cnt + (int)threadIdx.x; p < w; p += kCommitThreads) {
             r.fid_w[f0 + p] = -1;
             r.active[f0 + p] = 0;
         }
@@ -1556,11 +1603,11 @@ static int launch_repack(const Plan &P, int f0, int h) {
     r.fid_w = P.w.rs.fid;
     const int64_t rows = code->E + 2 * code->V + code->C;
     ProfScope ps("repack", P.s);
-    // 1 024 workgroups (4 per CU) walk the rows; when the device decides not to repack they all
-    // leave at once (a few microseconds on the variable stream)
-    k_repack_rows<<<(unsigned)std::min<int64_t>(rows, 1024), kRepackThreads, 0, P.s>>>(r);
+    // kRepackGrid workgroups walk the rows; when the device decides not to repack they all leave
+    // at once (a few microseconds on the variable stream)
+    k_repack_rows<<<(unsigned)std::min<int64_t>(rows, kRepackGrid), kRepackThreads, 0, P.s>>>(r);
     QR_LAUNCH_CHECK();
-    k_repack_commit<<<1, 1024, 0, P.s>>>(r);
+    k_repack_commit<<<1, kCommitThreads, 0, P.s>>>(r);
     QR_LAUNCH_CHECK();
     return QR_OK;
 }

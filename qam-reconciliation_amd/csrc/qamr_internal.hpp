@@ -104,6 +104,7 @@ struct qr_code {
     std::vector<DegreeClass> classes;
     int64_t fb_rows = 0;  // rows of the F scratch (sum over runtime-degree classes)
     qr::GlibcTables *d_gtab = nullptr; // strict box-plus: glibc exp/log data (glibc_math.hpp)
+    uint32_t *d_cu_arrivals = nullptr; // per-CU arrival counters of the frame-resident decode (knob res_stagger)
     mutable qr::Scratch scratch;
     // two-stream schedule (decoder.hip run_split2): a second stream for the variable
     // sweeps and the events that order the two; created on first use, guarded by mu

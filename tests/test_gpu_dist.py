@@ -31,7 +31,7 @@ def test_bench_rank_body_over_rccl(gpu):
     env.pop("QAMR_BENCH_STUB", None)
     env.pop("QAMR_BENCH_BACKEND", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--workload", "reg1008_4pam",
-           "--batch", "256", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0", "--no-alt",
+           "--batch", "256", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0",
            "--no-secondary", "--no-roofline"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
