@@ -1,6 +1,7 @@
 #!/bin/bash
-# Round-5 evidence: kernel trace + PMC passes of the default bench (4-PAM headline) and
-# PMC passes of the 16-PAM workload's demapper; summaries -> gpurun_out/prof_r05*/.
+# Round-5 evidence: kernel trace + PMC passes of the default bench (4-PAM headline) and of the
+# 16-PAM workload (its demapper), kernel traces of configs[1] and of the 4-PAM 4.0 dB converging
+# point; summaries -> gpurun_out/prof_r05*/.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -16,5 +17,7 @@ bash scripts/profile_session.sh || exit 1
 python3 scripts/summarize_profile.py gpurun_out/prof_${PTAG:-r05}_16pam --kernel 'k_demap_wave<4>' --kernel-key demap \
     --workload dvbs2_16pam > /dev/null || exit 1
 TAG=${PTAG:-r05}_configs1 TRACE_ARGS="--workload reg1008_4pam --batch 1024 --steps 5 --warmup 1 --cpu-seconds 0 --no-secondary" \
+SKIP_PMC=1 bash scripts/profile_session.sh || exit 1
+TAG=${PTAG:-r05}_4db TRACE_ARGS="--snr 4.0 --steps 2 --warmup 1 --cpu-seconds 0 --no-secondary" \
 SKIP_PMC=1 bash scripts/profile_session.sh || exit 1
 echo done
