@@ -945,12 +945,11 @@ __global__ void __launch_bounds__(1024) k_compact(int f0, int f1, uint8_t *__res
 // The decision points run on the variable stream beside the other range's check launch, whose
 // waves hold 4 x 120 of the 512 VGPRs of a SIMD: the repack waves must fit in the 32 left, or
 // their workgroups are dispatched only as check workgroups retire (a first 48-VGPR version waited
-// ~0.26 ms per decision point at 4-PAM 4.0 dB).  So each workgroup owns whole rows, takes its
-// chunk's source columns from the list once (kRepackPer per thread, in registers for all of its
-// rows) and moves two rows per barrier: 2 x kRepackPer loads in flight per thread, the row base in
-// scalar registers and the column as a 32-bit offset.
+// ~0.26 ms per decision point at 4-PAM 4.0 dB).  So the chunk's slots (source and destination
+// element offsets) are computed once and held in registers for all of a workgroup's rows, and
+// loads and stores are raw buffer accesses off a scalar base.
 constexpr int kRepackThreads = 256;
-constexpr int kRepackPer = 4;  // columns per thread per chunk
+constexpr int kRepackPer = 4;  // slots per thread per chunk
 constexpr int kRepackChunk = kRepackThreads * kRepackPer;
 constexpr int kRepackGrid = 512;  // workgroups of k_repack_rows (2 per CU)
 
@@ -987,12 +986,12 @@ __device__ __forceinline__ void loads_done_barrier() {
     __syncthreads();
 }
 
-// Raw buffer access to one row of a frame-innermost array (row base in scalar registers, the lane's
-// byte offset in a VGPR): an offset past the row reads 0 and drops the store, so slots past the
-// count need no branch.
+// Raw buffer access to a run of rows of a frame-innermost array (base in scalar registers, the
+// lane's byte offset in a VGPR): an offset past the run reads 0 and drops the store, so empty slots
+// need no branch.
 template <typename T>
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc_of(const T *rowp, int ld) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(rowp), (short)0, ld * (int)sizeof(T), 0x00020000);
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const T *p, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(p), (short)0, bytes, 0x00020000);
 }
 __device__ __forceinline__ double rb_load(__amdgpu_buffer_rsrc_t r, uint32_t off, double) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
@@ -1007,74 +1006,79 @@ __device__ __forceinline__ void rb_store(__amdgpu_buffer_rsrc_t r, uint32_t off,
     __builtin_amdgcn_raw_buffer_store_b8(v, r, off, 0, 0);
 }
 
-// One chunk of this workgroup's rows r = blockIdx.x + k gridDim.x < nrows of one array: element
-// (row, dcol0 + u * 256 + tid) <- (row, col[u]) for the slots with bit u of has, two rows per
-// barrier.
+// One chunk of one array's rows for this workgroup, which owns the contiguous rows [ra, rb) of it.
+// The chunk's slots (u, tid) -> (row j of a group of rg consecutive rows, column p0 + q): element
+// (row, f0 + p0 + q) <- (row, list[f0 + p0 + q]); groups of rg rows (rg > 1 when the count is small,
+// so a barrier moves several short rows), one group per barrier.  src_el / dst_el: the slots'
+// byte offsets inside a group of double rows (8 (j ld + column)), kRepackNone for an empty slot.
+constexpr uint32_t kRepackNone = 0xFFFFFFF0u;  // past any group: loads 0, stores nothing
 template <typename T>
-__device__ __forceinline__ void compact_rows(const T *src, T *dst, int64_t nrows, int ld, int dcol0,
-                                             const uint32_t (&col)[kRepackPer], uint32_t has) {
-    constexpr uint32_t kNone = 0xFFFFFFF0u;  // past any row: loads 0, stores nothing
-    // col[u] already holds the byte offset of the source column, or kNone (see k_repack_rows)
-    const uint32_t dbase = (uint32_t)(dcol0 + (int)threadIdx.x) * (uint32_t)sizeof(T);
-    const int64_t G = gridDim.x;
-    for (int64_t r0 = blockIdx.x; r0 < nrows; r0 += 2 * G) {
-        const int64_t r1 = r0 + G;
-        const bool two = r1 < nrows;  // block-uniform
-        const auto s0 = row_rsrc_of(src + (size_t)r0 * ld, ld);
-        const auto s1 = row_rsrc_of(src + (size_t)(two ? r1 : r0) * ld, ld);
-        T v0[kRepackPer], v1[kRepackPer];
+__device__ __forceinline__ void compact_rows(const T *src, T *dst, int64_t ra, int64_t rb, int ld, int rg,
+                                             const uint32_t (&src_el)[kRepackPer],
+                                             const uint32_t (&dst_el)[kRepackPer]) {
+    for (int64_t g0 = ra; g0 < rb; g0 += rg) {
+        const int n0 = (int)min<int64_t>(rg, rb - g0);  // block-uniform
+        const auto s0 = make_rsrc(src + (size_t)g0 * ld, n0 * ld * (int)sizeof(T));
+        T v0[kRepackPer];
 #pragma unroll
-        for (int u = 0; u < kRepackPer; ++u) {
-            const uint32_t so = col[u] == kNone ? kNone : col[u] / (8u / (uint32_t)sizeof(T));
-            v0[u] = rb_load(s0, so, T(0));
-            v1[u] = rb_load(s1, so, T(0));
-        }
+        for (int u = 0; u < kRepackPer; ++u) v0[u] = rb_load(s0, src_el[u] >> (sizeof(T) == 8 ? 0 : 3), T(0));
         loads_done_barrier();
-        const auto d0 = row_rsrc_of(dst + (size_t)r0 * ld, ld);
-        const auto d1 = row_rsrc_of(dst + (size_t)(two ? r1 : r0) * ld, ld);
+        const auto d0 = make_rsrc(dst + (size_t)g0 * ld, n0 * ld * (int)sizeof(T));
 #pragma unroll
-        for (int u = 0; u < kRepackPer; ++u) {
-            const uint32_t dof = ((has >> u) & 1u) ? dbase + (uint32_t)(u * kRepackThreads * sizeof(T)) : kNone;
-            rb_store(d0, dof, v0[u]);
-            if (two) rb_store(d1, dof, v1[u]);
-        }
+        for (int u = 0; u < kRepackPer; ++u) rb_store(d0, dst_el[u] >> (sizeof(T) == 8 ? 0 : 3), v0[u]);
     }
 }
 
-// The row moves of a repack: messages in place, posteriors / LAPPRs / syndrome bytes from the
-// caller's arrays (first repack) or in place in the work set; each array's rows are owned by
-// workgroup (row mod gridDim.x) through every chunk, so a row's chunks run in ascending order.
+// this workgroup's contiguous share [ra, rb) of n rows
+__device__ __forceinline__ void row_share(int64_t n, int64_t &ra, int64_t &rb) {
+    ra = n * blockIdx.x / gridDim.x;
+    rb = n * (blockIdx.x + 1) / gridDim.x;
+}
+
+// The row moves of a repack: messages in place, LAPPRs / syndrome bytes from the caller's arrays
+// (first repack) or in place in the work set.  Posteriors are not moved: the range's variable sweep
+// right after rewrites every running frame's posterior in its new column; only the frames stopped
+// since the last repack hand theirs (in the work set) to the output first.  Each array's rows are
+// split into contiguous shares, one per workgroup for every chunk, so a row's chunks run in
+// ascending order.
 __global__ void __launch_bounds__(kRepackThreads) k_repack_rows(RepackArgs r) {
     int cnt, w, w_new;
     if (!repack_go(r, cnt, w, w_new)) return;  // kernel-uniform
     const bool on = sld(r.sel + kSelOn) != 0;
     const size_t ld = r.ld;
     const int f0 = r.f0;
+    int64_t ra, rb;
     if (on) {  // frames stopped since the last repack hand their posteriors to the output first
-        for (int64_t v = blockIdx.x; v < r.V; v += gridDim.x) {
+        row_share(r.V, ra, rb);
+        for (int64_t v = ra; v < rb; ++v) {
             const double *src = r.post_w + (size_t)v * ld + f0;
             for (int q = threadIdx.x; q < w; q += kRepackThreads) {
                 const int id = r.fid_w[f0 + q];
                 if (id >= 0 && !r.active[f0 + q]) r.out_post[(size_t)v * ld + id] = src[q];
             }
         }
-        loads_done_barrier();  // (every such read before any compaction write below)
     }
+    // a small count moves several rows per group: rg rows x cnt columns fill the chunk's slots
+    const int rg = cnt <= kRepackChunk / 2 ? min(16, kRepackChunk / cnt) : 1;
     for (int p0 = 0; p0 < cnt; p0 += kRepackChunk) {
-        // the chunk's source columns as byte offsets of a double row (a byte row divides by 8),
-        // kNone past the count
-        uint32_t col[kRepackPer], has = 0;
+        const int pc = min(cnt - p0, kRepackChunk);  // columns of this chunk (rg = 1 unless one chunk)
+        uint32_t src_el[kRepackPer], dst_el[kRepackPer];
 #pragma unroll
         for (int u = 0; u < kRepackPer; ++u) {
-            const int p = p0 + u * kRepackThreads + (int)threadIdx.x;
-            col[u] = p < cnt ? (uint32_t)r.list[f0 + p] * 8u : 0xFFFFFFF0u;
-            has |= (p < cnt ? 1u : 0u) << u;
+            const int sl = u * kRepackThreads + (int)threadIdx.x;
+            const int j = sl / pc, q = sl - j * pc;
+            const bool ok = j < rg;
+            // byte offsets in a double row group (a byte row group shifts them right by 3; an empty
+            // slot's offset stays past the group either way)
+            src_el[u] = ok ? (uint32_t)(j * (int)ld + r.list[f0 + p0 + q]) * 8u : kRepackNone;
+            dst_el[u] = ok ? (uint32_t)(j * (int)ld + f0 + p0 + q) * 8u : kRepackNone;
         }
-        const int dcol0 = f0 + p0;
-        compact_rows<double>(r.c2v, r.c2v, r.E, r.ld, dcol0, col, has);
-        compact_rows<double>(on ? r.post_w : r.out_post, r.post_w, r.V, r.ld, dcol0, col, has);
-        compact_rows<double>(on ? r.lappr_w : r.lappr_in, r.lappr_w, r.V, r.ld, dcol0, col, has);
-        compact_rows<uint8_t>(on ? r.synd_w : r.synd_in, r.synd_w, r.C, r.ld, dcol0, col, has);
+        row_share(r.E, ra, rb);
+        compact_rows<double>(r.c2v, r.c2v, ra, rb, r.ld, rg, src_el, dst_el);
+        row_share(r.V, ra, rb);
+        compact_rows<double>(on ? r.lappr_w : r.lappr_in, r.lappr_w, ra, rb, r.ld, rg, src_el, dst_el);
+        row_share(r.C, ra, rb);
+        compact_rows<uint8_t>(on ? r.synd_w : r.synd_in, r.synd_w, ra, rb, r.ld, rg, src_el, dst_el);
     }
 }
 
@@ -1214,7 +1218,7 @@ struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3},
         lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024}, var_pace{28},
         check_tail{4}, fused_iter{1}, iter_streams{2}, var_boost{4}, resident{1}, repack{1},
-        repack_pct{75};
+        repack_pct{50};
 };
 static Tuning g_tune;
 
