@@ -368,6 +368,94 @@ __device__ __forceinline__ void var_block(const VarArgs &a, unsigned bx, unsigne
     if (INIT && a.finite && big && f < a.fin_B) *a.finite = 0;  // every writer stores 0
 }
 
+// ---------------------------------------------------------------------------------------
+// Narrow sweeps: a repacked range of at most kNarrowW columns (the last running frames of a
+// converging half).  The frame-parallel layout gives every check a 64-lane wave of frames, so
+// a handful of running frames still pay a whole wave per check, per checks in sequence.  Such
+// a range (known only on the device: its RangeSel) switches the SAME launch, kernel-uniformly,
+// to lanes = (node, frame): a workgroup task is kNarrowNodes nodes x kNarrowFrames consecutive
+// columns (one 128-byte line per row access), one node per lane, tasks walked grid-stride, the
+// CSR read per lane.  Every message is the same operation on the same operands as in
+// check_block / var_block, so the bits do not depend on the layout.
+constexpr int kNarrowFrames = 16;
+constexpr int kNarrowNodes = 256 / kNarrowFrames;
+constexpr int kNarrowW = 64;
+
+__device__ __forceinline__ bool range_narrow(const int32_t *sel, const int32_t *acount) {
+    return sel && acount && sld(sel + kSelOn) && sld(sel + kSelW) <= kNarrowW;
+}
+// Tasks of a narrow sweep over n nodes: (node block, frame group) pairs, frame group fastest.
+__device__ __forceinline__ int64_t narrow_tasks(int64_t n, const int32_t *acount, int &ngrp) {
+    ngrp = (sld(acount) + kNarrowFrames - 1) / kNarrowFrames;
+    return (n + kNarrowNodes - 1) / kNarrowNodes * ngrp;
+}
+
+// The NaN-preserving clamp always (the finite flag's one-instruction clamp gives the same bits
+// on finite inputs; the narrow body is not worth a second copy).
+template <int D>
+__device__ __forceinline__ void check_narrow(const CheckArgs &a, int64_t task, int ngrp, const GlibcTablesBP &tab,
+                                             double *hb, const GlibcK &K) {
+    bool live;
+    const int grp = (int)(task % ngrp);
+    const int f = lane_frame(a.alist, a.acount, a.f_off, grp * kNarrowFrames + (int)(threadIdx.x % kNarrowFrames), live);
+    const bool act = live && a.active[f] != 0;
+    if (!wave_any(act)) return;  // wave-uniform: the packed update exchanges within the wave
+    const int64_t ci = task / ngrp * kNarrowNodes + threadIdx.x / kNarrowFrames;
+    const bool valid = ci < a.n_checks;
+    const int cc = a.checks[valid ? ci : a.n_checks - 1];
+    int base = a.chk_ptr[cc];
+    const size_t ld = a.ld;
+    const uint8_t sb = a.synd[(size_t)cc * ld + f];
+    uint32_t par = sb;
+    double m[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        const double p = a.post[(size_t)a.chk_var[base + i] * ld + f];
+        par ^= (p < 0.0) ? 1u : 0u;                                // decoder.pyx:243-246
+        m[i] = p - a.c2v[(size_t)a.chk_edge[base + i] * ld + f];  // :296-297
+    }
+    double out[D];
+    check_strict_packed<D, kClampFull>(m, out, hb + (threadIdx.x >> 6) * kPackWaveDoubles, tab, K);
+    // the stores re-read the edge ids: D message addresses held across the update would raise
+    // the kernel's register budget (its frame-parallel body runs at 4 waves/SIMD)
+    __asm__ volatile("" : "+v"(base));
+    const double s = sb ? -1.0 : 1.0;
+    if (valid && act) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) a.c2v[(size_t)a.chk_edge[base + i] * ld + f] = s * out[i];
+        if (par == 1u) a.unsat[f] = 1;  // benign race: every writer stores 1
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void check_narrow_sweep(const CheckArgs &a, GlibcTablesBP &tab, double *hb) {
+    int ngrp;
+    const int64_t ntask = narrow_tasks(a.n_checks, a.acount, ngrp);
+    const unsigned nb = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x;
+    if (b >= ntask) return;  // block-uniform
+    stage_glibc_tables(&tab, a.gglibc);
+    const auto K = GlibcK::pinned();
+    for (int64_t t = b; t < ntask; t += nb) check_narrow<D>(a, t, ngrp, tab, hb, K);
+}
+
+__device__ __forceinline__ void var_narrow_sweep(const VarArgs &a) {
+    int ngrp;
+    const int64_t ntask = narrow_tasks(a.V, a.acount, ngrp);
+    const unsigned nb = gridDim.x * gridDim.y;
+    const size_t ld = a.ld;
+    for (int64_t t = blockIdx.y * gridDim.x + blockIdx.x; t < ntask; t += nb) {
+        bool live;
+        const int grp = (int)(t % ngrp);
+        const int f = lane_frame(a.alist, a.acount, a.f_off, grp * kNarrowFrames + (int)(threadIdx.x % kNarrowFrames), live);
+        const int64_t v = t / ngrp * kNarrowNodes + threadIdx.x / kNarrowFrames;
+        if (!live || v >= a.V || !a.active[f]) continue;
+        double p = a.lappr[(size_t)v * ld + f];
+        const int b = a.var_ptr[v], e = a.var_ptr[v + 1];
+        for (int k = b; k < e; ++k) p += a.c2v[(size_t)a.var_edge[k] * ld + f];  // decoder.pyx:292-293
+        a.post[(size_t)v * ld + f] = p;
+    }
+}
+
 // QR_EXPERIMENT_CLOCK (diagnostic builds only, scripts/diag/clock_check.py): every workgroup of
 // the degree-7 main-loop check sweep stamps the shader clock (s_memtime) and the 100 MHz
 // realtime counter around its work and adds both spans to g_clk (vector atomics); the effective
@@ -410,6 +498,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
     __shared__ GlibcTablesBP tab;
     __shared__ double hb[kPackLdsDoubles];
     select_range(a);
+    if constexpr (MODE == kNormal && kPacked<D>) {
+        if (range_narrow(a.sel, a.acount)) {  // kernel-uniform
+            check_narrow_sweep<D>(a, tab, hb);
+            return;
+        }
+    }
     unsigned bx = blockIdx.x, by = blockIdx.y;
     int per = a.g.per;
     if (a.nmain) {  // short-tail 1-D grid (block-uniform)
@@ -439,6 +533,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
 template <bool INIT, bool NT>
 __global__ void __launch_bounds__(256) k_var(VarArgs a) {
     select_range(a);
+    if (!INIT && range_narrow(a.sel, a.acount)) {  // kernel-uniform
+        var_narrow_sweep(a);
+        return;
+    }
     if (a.gs) {  // capped grid: tile t = (bx fastest, by), the grid's blocks sweep a moving window
         unsigned ny = a.nby, stride = gridDim.x;
         if (a.boost > 1) {
@@ -586,6 +684,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
 // traffic for the messages.  In LDS message (c, i) lives at i C + c, so the lanes of a check
 // phase (consecutive checks) touch consecutive doubles.  Workgroup b takes frame (b % 8) ceil(B / 8) + b / 8, so the frames
 // of one XCD are contiguous columns and their LAPPR sectors stay in that XCD's L2.
+#ifndef QR_RES_PRE
+#define QR_RES_PRE 1
+#endif
+#ifndef QR_RES_LREG
+#define QR_RES_LREG 1
+#endif
 constexpr int kResThreads = 512;
 constexpr int kResMaxIter = 10000;  // one launch runs every iteration: bound its length
 constexpr int kResStaticLds = (int)sizeof(GlibcTablesBP) + (kResThreads / 64) * kPackWaveDoubles * 8;
@@ -633,12 +737,17 @@ __device__ __forceinline__ void resident_loop(const ResArgs &a, int f, double *m
     // the first check of this thread (all of them when C <= kResThreads): its variables and
     // syndrome bit stay in registers across the iterations (D <= 6: within 128 VGPRs; above,
     // the indices would spill and are re-read from L1 instead)
-    constexpr bool kPre = D <= 6;
+    constexpr bool kPre = QR_RES_PRE && D <= 6;
     const int c_first = min(tid, a.C - 1);
     int pv[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) pv[i] = kPre ? a.chk_var[c_first * D + i] : 0;
     const uint8_t sb_first = a.synd[(size_t)c_first * ld + f];
+    // the LAPPRs of this lane's (at most two) variables stay in registers when V <= 2 x 512
+    // (configs[1]: 1 008), instead of an L2 read per variable per iteration
+    const bool lreg = QR_RES_LREG && a.V <= 2 * kResThreads;  // block-uniform
+    const double l0 = lreg && tid < a.V ? a.lappr[(size_t)tid * ld + f] : 0.0;
+    const double l1 = lreg && tid + kResThreads < a.V ? a.lappr[(size_t)(tid + kResThreads) * ld + f] : 0.0;
     for (int t = 1; t <= a.max_it; ++t) {
         uint32_t bad = 0;
         for (int c0 = 0; c0 < a.C; c0 += kResThreads) {
@@ -676,8 +785,8 @@ __device__ __forceinline__ void resident_loop(const ResArgs &a, int f, double *m
             const int v1 = v0 + kResThreads;
             const bool two = v1 < a.V;
             const int w1 = two ? v1 : v0;
-            double p0 = a.lappr[(size_t)v0 * ld + f];
-            double p1 = a.lappr[(size_t)w1 * ld + f];
+            double p0 = lreg ? l0 : a.lappr[(size_t)v0 * ld + f];
+            double p1 = lreg ? l1 : a.lappr[(size_t)w1 * ld + f];
             const int b0 = a.var_ptr[v0], e0 = a.var_ptr[v0 + 1];
             const int b1 = a.var_ptr[w1], e1 = a.var_ptr[w1 + 1];
             const int n = max(e0 - b0, e1 - b1);
@@ -1580,7 +1689,8 @@ static int side_stream(const qr_code *code, hipStream_t *out) {
     return QR_OK;
 }
 
-// A repack decision point of the range starting at column f0 (full width h), on P.s: the device
+// A repack decision point of the range starting at column f0 (full width h), on P.s (the variable
+// stream): the device
 // decides and, when it repacks, moves the columns (k_repack_rows) and updates the range's state
 // (k_repack_commit).
 static int launch_repack(const Plan &P, int f0, int h) {
@@ -1615,6 +1725,17 @@ static int launch_repack(const Plan &P, int f0, int h) {
     QR_LAUNCH_CHECK();
     return QR_OK;
 }
+
+#ifndef QR_EXPERIMENT_NOP
+#define QR_EXPERIMENT_NOP 0
+#endif
+#if QR_EXPERIMENT_NOP
+// diagnostic builds only (scripts/exp_build.sh): empty launches on the variable stream before each
+// variable sweep, to price a launch boundary beside the check sweep
+__global__ void k_nop(const int32_t *count) {
+    if (sld(count) < -1) __builtin_trap();
+}
+#endif
 
 // *finalized: the final parity check, status and output were issued here (device-steered repack).
 static int run_split2(const Plan &P, int max_it, bool *finalized) {
@@ -1670,6 +1791,9 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
     // launch
     auto var_sweep = [&](int k) {
         const int f0 = k * h;
+#if QR_EXPERIMENT_NOP
+        for (int i = 0; i < QR_EXPERIMENT_NOP; ++i) k_nop<<<kRepackGrid, kRepackThreads, 0, V.s>>>(P.w.acount);
+#endif
         if (rp) {
             if (int rc0 = launch_repack(V, f0, h)) return rc0;
         }
