@@ -384,23 +384,26 @@ constexpr int kNarrowW = 64;
 __device__ __forceinline__ bool range_narrow(const int32_t *sel, const int32_t *acount) {
     return sel && acount && sld(sel + kSelOn) && sld(sel + kSelW) <= kNarrowW;
 }
-// Tasks of a narrow sweep over n nodes: (node block, frame group) pairs, frame group fastest.
-__device__ __forceinline__ int64_t narrow_tasks(int64_t n, const int32_t *acount, int &ngrp) {
-    ngrp = (sld(acount) + kNarrowFrames - 1) / kNarrowFrames;
-    return (n + kNarrowNodes - 1) / kNarrowNodes * ngrp;
+// Tasks of a narrow sweep over n nodes: (node block, frame group) pairs, frame group fastest, the
+// group count (<= 4) rounded up to 2^lg so that a task splits with a shift and a mask (32-bit task
+// arithmetic: the variable sweep keeps its register budget)
+__device__ __forceinline__ uint32_t narrow_tasks(int64_t n, const int32_t *acount, int &lg) {
+    const int ngrp = (sld(acount) + kNarrowFrames - 1) / kNarrowFrames;
+    lg = ngrp > 2 ? 2 : ngrp > 1 ? 1 : 0;
+    return ngrp > 0 ? (uint32_t)((n + kNarrowNodes - 1) / kNarrowNodes) << lg : 0u;
 }
 
 // The NaN-preserving clamp always (the finite flag's one-instruction clamp gives the same bits
 // on finite inputs; the narrow body is not worth a second copy).
 template <int D>
-__device__ __forceinline__ void check_narrow(const CheckArgs &a, int64_t task, int ngrp, const GlibcTablesBP &tab,
+__device__ __forceinline__ void check_narrow(const CheckArgs &a, uint32_t task, int lg, const GlibcTablesBP &tab,
                                              double *hb, const GlibcK &K) {
     bool live;
-    const int grp = (int)(task % ngrp);
+    const int grp = (int)(task & ((1u << lg) - 1u));
     const int f = lane_frame(a.alist, a.acount, a.f_off, grp * kNarrowFrames + (int)(threadIdx.x % kNarrowFrames), live);
     const bool act = live && a.active[f] != 0;
     if (!wave_any(act)) return;  // wave-uniform: the packed update exchanges within the wave
-    const int64_t ci = task / ngrp * kNarrowNodes + threadIdx.x / kNarrowFrames;
+    const int64_t ci = (int64_t)(task >> lg) * kNarrowNodes + threadIdx.x / kNarrowFrames;
     const bool valid = ci < a.n_checks;
     const int cc = a.checks[valid ? ci : a.n_checks - 1];
     int base = a.chk_ptr[cc];
@@ -429,25 +432,25 @@ __device__ __forceinline__ void check_narrow(const CheckArgs &a, int64_t task, i
 
 template <int D>
 __device__ __forceinline__ void check_narrow_sweep(const CheckArgs &a, GlibcTablesBP &tab, double *hb) {
-    int ngrp;
-    const int64_t ntask = narrow_tasks(a.n_checks, a.acount, ngrp);
-    const unsigned nb = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x;
+    int lg;
+    const uint32_t ntask = narrow_tasks(a.n_checks, a.acount, lg);
+    const uint32_t nb = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x;
     if (b >= ntask) return;  // block-uniform
     stage_glibc_tables(&tab, a.gglibc);
     const auto K = GlibcK::pinned();
-    for (int64_t t = b; t < ntask; t += nb) check_narrow<D>(a, t, ngrp, tab, hb, K);
+    for (uint32_t t = b; t < ntask; t += nb) check_narrow<D>(a, t, lg, tab, hb, K);
 }
 
 __device__ __forceinline__ void var_narrow_sweep(const VarArgs &a) {
-    int ngrp;
-    const int64_t ntask = narrow_tasks(a.V, a.acount, ngrp);
-    const unsigned nb = gridDim.x * gridDim.y;
+    int lg;
+    const uint32_t ntask = narrow_tasks(a.V, a.acount, lg);
+    const uint32_t nb = gridDim.x * gridDim.y;
     const size_t ld = a.ld;
-    for (int64_t t = blockIdx.y * gridDim.x + blockIdx.x; t < ntask; t += nb) {
+    for (uint32_t t = blockIdx.y * gridDim.x + blockIdx.x; t < ntask; t += nb) {
         bool live;
-        const int grp = (int)(t % ngrp);
+        const int grp = (int)(t & ((1u << lg) - 1u));
         const int f = lane_frame(a.alist, a.acount, a.f_off, grp * kNarrowFrames + (int)(threadIdx.x % kNarrowFrames), live);
-        const int64_t v = t / ngrp * kNarrowNodes + threadIdx.x / kNarrowFrames;
+        const int64_t v = (int64_t)(t >> lg) * kNarrowNodes + threadIdx.x / kNarrowFrames;
         if (!live || v >= a.V || !a.active[f]) continue;
         double p = a.lappr[(size_t)v * ld + f];
         const int b = a.var_ptr[v], e = a.var_ptr[v + 1];
@@ -684,12 +687,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
 // traffic for the messages.  In LDS message (c, i) lives at i C + c, so the lanes of a check
 // phase (consecutive checks) touch consecutive doubles.  Workgroup b takes frame (b % 8) ceil(B / 8) + b / 8, so the frames
 // of one XCD are contiguous columns and their LAPPR sectors stay in that XCD's L2.
-#ifndef QR_RES_PRE
-#define QR_RES_PRE 1
-#endif
-#ifndef QR_RES_LREG
-#define QR_RES_LREG 1
-#endif
 constexpr int kResThreads = 512;
 constexpr int kResMaxIter = 10000;  // one launch runs every iteration: bound its length
 constexpr int kResStaticLds = (int)sizeof(GlibcTablesBP) + (kResThreads / 64) * kPackWaveDoubles * 8;
@@ -737,7 +734,7 @@ __device__ __forceinline__ void resident_loop(const ResArgs &a, int f, double *m
     // the first check of this thread (all of them when C <= kResThreads): its variables and
     // syndrome bit stay in registers across the iterations (D <= 6: within 128 VGPRs; above,
     // the indices would spill and are re-read from L1 instead)
-    constexpr bool kPre = QR_RES_PRE && D <= 6;
+    constexpr bool kPre = D <= 6;
     const int c_first = min(tid, a.C - 1);
     int pv[D];
 #pragma unroll
@@ -745,7 +742,7 @@ __device__ __forceinline__ void resident_loop(const ResArgs &a, int f, double *m
     const uint8_t sb_first = a.synd[(size_t)c_first * ld + f];
     // the LAPPRs of this lane's (at most two) variables stay in registers when V <= 2 x 512
     // (configs[1]: 1 008), instead of an L2 read per variable per iteration
-    const bool lreg = QR_RES_LREG && a.V <= 2 * kResThreads;  // block-uniform
+    const bool lreg = a.V <= 2 * kResThreads;  // block-uniform
     const double l0 = lreg && tid < a.V ? a.lappr[(size_t)tid * ld + f] : 0.0;
     const double l1 = lreg && tid + kResThreads < a.V ? a.lappr[(size_t)(tid + kResThreads) * ld + f] : 0.0;
     for (int t = 1; t <= a.max_it; ++t) {
@@ -1057,6 +1054,13 @@ __global__ void __launch_bounds__(1024) k_compact(int f0, int f1, uint8_t *__res
 // ~0.26 ms per decision point at 4-PAM 4.0 dB).  So the chunk's slots (source and destination
 // element offsets) are computed once and held in registers for all of a workgroup's rows, and
 // loads and stores are raw buffer accesses off a scalar base.
+// Register note (MI355X, measured, mechanism not established): the kernels launched beside the
+// check waves (120 VGPRs allocated, 4 per SIMD) must allocate 16 or 32 VGPRs, not 24.  With this
+// kernel at 24 (22 used) every dense iteration ran slower, although at a dense iteration it only
+// reads two words and exits: headline 9 547 vs 9 790 frames/s (same box, alternating runs), 9 798
+// with the round's earlier 28-VGPR version; a variable sweep at 24 (18 used) cost the same
+// (9 552 vs 9 776).  So k_repack_rows allocates 32 (an empty asm clobbering v31) and k_var stays
+// at 16 (32-bit task arithmetic in its narrow sweep).
 constexpr int kRepackThreads = 256;
 constexpr int kRepackPer = 4;  // slots per thread per chunk
 constexpr int kRepackChunk = kRepackThreads * kRepackPer;
@@ -1152,6 +1156,8 @@ __device__ __forceinline__ void row_share(int64_t n, int64_t &ra, int64_t &rb) {
 // ascending order.
 __global__ void __launch_bounds__(kRepackThreads) k_repack_rows(RepackArgs r) {
     int cnt, w, w_new;
+    // allocate 32 VGPRs (the code needs 22): see the register note above
+    __asm__ volatile("" ::: "v31");
     if (!repack_go(r, cnt, w, w_new)) return;  // kernel-uniform
     const bool on = sld(r.sel + kSelOn) != 0;
     const size_t ld = r.ld;
@@ -1190,6 +1196,7 @@ __global__ void __launch_bounds__(kRepackThreads) k_repack_rows(RepackArgs r) {
         compact_rows<uint8_t>(on ? r.synd_w : r.synd_in, r.synd_w, ra, rb, r.ld, rg, src_el, dst_el);
     }
 }
+
 
 // One workgroup (4 waves, one per SIMD) after k_repack_rows: frame ids, list, active flags and the
 // RangeSel.
@@ -1726,17 +1733,6 @@ static int launch_repack(const Plan &P, int f0, int h) {
     return QR_OK;
 }
 
-#ifndef QR_EXPERIMENT_NOP
-#define QR_EXPERIMENT_NOP 0
-#endif
-#if QR_EXPERIMENT_NOP
-// diagnostic builds only (scripts/exp_build.sh): empty launches on the variable stream before each
-// variable sweep, to price a launch boundary beside the check sweep
-__global__ void k_nop(const int32_t *count) {
-    if (sld(count) < -1) __builtin_trap();
-}
-#endif
-
 // *finalized: the final parity check, status and output were issued here (device-steered repack).
 static int run_split2(const Plan &P, int max_it, bool *finalized) {
     const qr_code *code = P.code;
@@ -1791,9 +1787,6 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
     // launch
     auto var_sweep = [&](int k) {
         const int f0 = k * h;
-#if QR_EXPERIMENT_NOP
-        for (int i = 0; i < QR_EXPERIMENT_NOP; ++i) k_nop<<<kRepackGrid, kRepackThreads, 0, V.s>>>(P.w.acount);
-#endif
         if (rp) {
             if (int rc0 = launch_repack(V, f0, h)) return rc0;
         }
