@@ -702,6 +702,7 @@ struct ResArgs {
     int32_t *iters;
     const GlibcTables *gglibc;
     double fin_bound;  // |lappr| below it for every variable -> the finite clamp (0: never)
+    int dv;            // every variable of degree dv <= 3 and E < 2^16 (0: otherwise)
 };
 
 // parity of the posteriors in LDS (decoder.pyx:235-257): 1 iff some check of this thread fails
@@ -731,20 +732,28 @@ __device__ __forceinline__ void resident_loop(const ResArgs &a, int f, double *m
     const int tid = threadIdx.x;
     const size_t ld = a.ld;
     const auto K = GlibcK::pinned();
-    // the first check of this thread (all of them when C <= kResThreads): its variables and
-    // syndrome bit stay in registers across the iterations (D <= 6: within 128 VGPRs; above,
-    // the indices would spill and are re-read from L1 instead)
-    constexpr bool kPre = D <= 6;
+    // the first check of this thread (all of them when C <= kResThreads): its syndrome bit stays
+    // in a register across the iterations (its variable indices are re-read from L1: pinning
+    // them too spilled with the variable phase's registers below, 907 k vs 911 k frames/s)
     const int c_first = min(tid, a.C - 1);
-    int pv[D];
-#pragma unroll
-    for (int i = 0; i < D; ++i) pv[i] = kPre ? a.chk_var[c_first * D + i] : 0;
     const uint8_t sb_first = a.synd[(size_t)c_first * ld + f];
     // the LAPPRs of this lane's (at most two) variables stay in registers when V <= 2 x 512
     // (configs[1]: 1 008), instead of an L2 read per variable per iteration
     const bool lreg = a.V <= 2 * kResThreads;  // block-uniform
     const double l0 = lreg && tid < a.V ? a.lappr[(size_t)tid * ld + f] : 0.0;
     const double l1 = lreg && tid + kResThreads < a.V ? a.lappr[(size_t)(tid + kResThreads) * ld + f] : 0.0;
+    // regular variable degree dv <= 3 (configs[1]: 3): the LDS message indices of those two
+    // variables' edges too, two 16-bit indices per register, instead of index loads per iteration
+    const int dv = lreg ? a.dv : 0;  // block-uniform
+    uint32_t vm[3] = {0u, 0u, 0u};
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        if (q < dv) {
+            const uint32_t i0 = tid < a.V ? (uint32_t)a.var_msg[tid * dv + q] : 0u;
+            const uint32_t i1 = tid + kResThreads < a.V ? (uint32_t)a.var_msg[(tid + kResThreads) * dv + q] : 0u;
+            vm[q] = i0 | i1 << 16;
+        }
+    }
     for (int t = 1; t <= a.max_it; ++t) {
         uint32_t bad = 0;
         for (int c0 = 0; c0 < a.C; c0 += kResThreads) {
@@ -757,7 +766,7 @@ __device__ __forceinline__ void resident_loop(const ResArgs &a, int f, double *m
             double m[D];
 #pragma unroll
             for (int i = 0; i < D; ++i) {
-                const double p = post[(kPre && c0 == 0) ? pv[i] : a.chk_var[cc * D + i]];
+                const double p = post[a.chk_var[cc * D + i]];
                 par ^= (p < 0.0) ? 1u : 0u;     // decoder.pyx:243-246
                 m[i] = p - msg[i * a.C + cc];    // :296-297
             }
@@ -778,7 +787,20 @@ __device__ __forceinline__ void resident_loop(const ResArgs &a, int f, double *m
         }
         // decoder.pyx:285-298, two variables per lane at a time: their (latency-bound, L1/L2)
         // LAPPR and index loads are issued together; each sum keeps its ascending edge order
-        for (int v0 = tid; v0 < a.V; v0 += 2 * kResThreads) {
+        if (dv) {  // block-uniform: LAPPRs and message indices in registers
+            double p0 = l0, p1 = l1;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                if (q < dv) {
+                    const double m0 = msg[vm[q] & 0xFFFFu], m1 = msg[vm[q] >> 16];
+                    p0 += m0;
+                    p1 += m1;
+                }
+            }
+            if (tid < a.V) post[tid] = p0;
+            if (tid + kResThreads < a.V) post[tid + kResThreads] = p1;
+        }
+        for (int v0 = dv ? a.V : tid; v0 < a.V; v0 += 2 * kResThreads) {
             const int v1 = v0 + kResThreads;
             const bool two = v1 < a.V;
             const int w1 = two ? v1 : v0;
@@ -1953,6 +1975,7 @@ static int run_resident(const qr_code *code, int B, int ld, const double *lappr,
     const double fin_x = ((double)max_it + 2.0) * std::log2((double)code->max_dv + 1.0);
     const int fin_e = fin_x > 999.0 ? 0 : 1000 - (int)std::ceil(fin_x);
     a.fin_bound = fin_e >= 1 ? std::ldexp(1.0, fin_e) : 0.0;
+    a.dv = code->reg_dv >= 1 && code->reg_dv <= 3 && code->E < 65536 ? code->reg_dv : 0;
     const unsigned grid = (unsigned)(8 * ((B + 7) / 8));
     const size_t lds = resident_lds(code);
     ProfScope ps(profiling_on() ? "resident_d" + std::to_string(code->classes[0].degree) : std::string(), s);
@@ -2160,6 +2183,9 @@ int qr_code_create(const int64_t *e_to_v, const int64_t *e_to_c, int64_t nv, int
     code->C = C;
     code->max_dc = max_dc;
     code->max_dv = max_dv;
+    code->reg_dv = max_dv;  // the common variable degree, or 0
+    for (int64_t v = 0; v < V; ++v)
+        if (var_ptr[(size_t)v + 1] - var_ptr[(size_t)v] != max_dv) code->reg_dv = 0;
     code->device = device;
     code->scratch.device = device;
     {

@@ -91,6 +91,7 @@ struct DegreeClass {
 struct qr_code {
     int64_t E = 0, V = 0, C = 0;
     int32_t max_dc = 0, max_dv = 0;
+    int32_t reg_dv = 0;  // every variable node's degree when they are all equal, else 0
     int device = 0;
     size_t mem_bytes = 0;       // the device's memory (bounds the optional repack work set)
     size_t lds_per_block = 0;   // LDS a workgroup may take (the frame-resident decode needs it)

@@ -199,7 +199,7 @@ def _check_regular_irregular_var(N, dc, seed):
     return sockets.astype(np.int64), np.repeat(np.arange(M), dc).astype(np.int64)
 
 
-@pytest.mark.parametrize("code", ["reg1008", "irr_d4", "irr_d7", "irr_d10"])
+@pytest.mark.parametrize("code", ["reg1008", "irr_d4", "irr_d7", "irr_d10", "reg_v1_d4", "reg_v2_d4"])
 def test_fused_iteration_schedule_vs_oracle(gpu, code):
     """Small codes decode in one frame-resident launch (k_resident: a workgroup per frame, its
     messages in LDS) or with one launch per iteration (k_iter: posteriors summed on the fly
@@ -212,6 +212,9 @@ def test_fused_iteration_schedule_vs_oracle(gpu, code):
 
     if code == "reg1008":
         vid, cid = codes.regular_code(1008)
+    elif code.startswith("reg_v"):  # regular variable degree 1 / 2 (the resident decode holds the
+        dv = int(code[5])          # edges' LDS indices in registers), V = 400 < 512 threads
+        vid, cid = codes.regular_code(400, dv=dv, dc=4, seed=10 + dv)
     else:
         dc = int(code.split("_d")[1])
         vid, cid = _check_regular_irregular_var(700, dc, seed=dc)
