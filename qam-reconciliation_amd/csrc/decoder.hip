@@ -166,10 +166,10 @@ struct VarArgs {
 };
 
 // The state of one frame range of the two-stream schedule, in device memory (the workspace's
-// count block), read by every launch of that range and written only by k_repack_commit: whether
+// count block), read by every launch of that range and written only by a repack's commit (k_repack_rows): whether
 // the range has moved to the repack work set, its width there (its running frames occupy the
 // first columns), and how many repacks it went through.
-enum RangeSelField { kSelOn = 0, kSelW = 1, kSelRepacks = 2, kSelInts = 4 };
+enum RangeSelField { kSelOn = 0, kSelW = 1, kSelRepacks = 2, kSelArrive = 3, kSelInts = 4 };
 
 // Kernel-uniform: the arrays a range's launch reads once the device has repacked the range.
 __device__ __forceinline__ void select_range(CheckArgs &a) {
@@ -1057,8 +1057,7 @@ __global__ void __launch_bounds__(1024) k_compact(int f0, int f1, uint8_t *__res
 //
 // Everything is decided on the device, so the decode stays asynchronous and capturable: at
 // each decision point (before a range's variable sweep, on the variable stream) k_repack_rows
-// and k_repack_commit read the range's running-frame count (written by its last status
-// launch) and its RangeSel; when the running frames fill at most pct % of the range's width w,
+// reads the range's running-frame count (written by its last status launch) and its RangeSel; when the running frames fill at most pct % of the range's width w,
 // the range moves to w' = max(64, count rounded up to 64):
 //   * messages: compacted in place in the workspace's c2v rows (the range's own columns);
 //   * posteriors, LAPPRs, syndrome bits: the first repack gathers them from the caller's arrays
@@ -1104,7 +1103,7 @@ struct RepackArgs {
     int32_t *fid_w;
 };
 
-// The decision, taken identically by every workgroup of k_repack_rows and by k_repack_commit
+// The decision, taken identically by every workgroup of k_repack_rows
 // (their inputs do not change between the two launches).
 __device__ __forceinline__ bool repack_go(const RepackArgs &r, int &cnt, int &w, int &w_new) {
     cnt = sld(r.count);
@@ -1170,6 +1169,36 @@ __device__ __forceinline__ void row_share(int64_t n, int64_t &ra, int64_t &rb) {
     rb = n * (blockIdx.x + 1) / gridDim.x;
 }
 
+// The commit of a repack (by the workgroup of k_repack_rows that finishes last): frame ids, list,
+// active flags and the RangeSel.
+__device__ __forceinline__ void repack_commit(const RepackArgs &r, int cnt, int w, int w_new, bool on) {
+    const int f0 = r.f0;
+    for (int p0 = 0; p0 < cnt; p0 += kRepackThreads) {
+        const int p = p0 + (int)threadIdx.x;
+        int id = 0;
+        if (p < cnt) {
+            const int sc = r.list[f0 + p];
+            id = on ? r.fid_w[sc] : sc;  // column = frame in the caller's arrays
+        }
+        loads_done_barrier();
+        if (p < cnt) {
+            r.fid_w[f0 + p] = id;
+            r.list[f0 + p] = f0 + p;
+            r.active[f0 + p] = 1;
+        }
+    }
+    for (int p = cnt + (int)threadIdx.x; p < w; p += kRepackThreads) {
+        r.fid_w[f0 + p] = -1;
+        r.active[f0 + p] = 0;
+    }
+    if (threadIdx.x == 0) {
+        r.sel[kSelOn] = 1;
+        r.sel[kSelW] = w_new;
+        r.sel[kSelRepacks] += 1;
+        r.sel[kSelArrive] = 0;
+    }
+}
+
 // The row moves of a repack: messages in place, LAPPRs / syndrome bytes from the caller's arrays
 // (first repack) or in place in the work set.  Posteriors are not moved: the range's variable sweep
 // right after rewrites every running frame's posterior in its new column; only the frames stopped
@@ -1217,45 +1246,17 @@ __global__ void __launch_bounds__(kRepackThreads) k_repack_rows(RepackArgs r) {
         row_share(r.C, ra, rb);
         compact_rows<uint8_t>(on ? r.synd_w : r.synd_in, r.synd_w, ra, rb, r.ld, rg, src_el, dst_el);
     }
+    // the workgroup that arrives last commits: every other one has read the list, frame ids and
+    // active flags it needed (its loads completed before its arrival), so the commit's rewrites of
+    // them race with nothing; the next launches see everything (kernel boundary)
+    __shared__ int last;
+    loads_done_barrier();
+    if (threadIdx.x == 0) last = atomicAdd(r.sel + kSelArrive, 1) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (last) repack_commit(r, cnt, w, w_new, on);
 }
 
 
-// One workgroup (4 waves, one per SIMD) after k_repack_rows: frame ids, list, active flags and the
-// RangeSel.
-constexpr int kCommitThreads = 256;
-__global__ void __launch_bounds__(kCommitThreads) k_repack_commit(RepackArgs r) {
-    int cnt, w, w_new;
-    const bool go = repack_go(r, cnt, w, w_new);
-    const bool on = sld(r.sel + kSelOn) != 0;
-    if (go) {
-        const int f0 = r.f0;
-        for (int p0 = 0; p0 < cnt; p0 += kCommitThreads) {
-            const int p = p0 + (int)threadIdx.x;
-            int id = 0;
-            if (p < cnt) {
-                const int sc = r.list[f0 + p];
-                id = on ? r.fid_w[sc] : sc;  // column = frame in the caller's arrays
-            }
-            loads_done_barrier();
-            if (p < cnt) {
-                r.fid_w[f0 + p] = id;
-                r.list[f0 + p] = f0 + p;
-                r.active[f0 + p] = 1;
-            }
-        }
-        for (int p = cnt + (int)threadIdx.x; p < w; p += kCommitThreads) {
-            r.fid_w[f0 + p] = -1;
-            r.active[f0 + p] = 0;
-        }
-    }
-    if (go && threadIdx.x == 0) {
-        r.sel[kSelOn] = 1;
-        r.sel[kSelW] = w_new;
-        r.sel[kSelRepacks] += 1;
-    }
-}
-
-// The end of the decode: every frame of a repacked range hands its posteriors to the output.
 __global__ void k_repack_output(int64_t rows, int f0, int ld, const int32_t *sel, const int32_t *__restrict__ fid_w,
                                 const double *__restrict__ post_w, double *__restrict__ out_post) {
     if (!sld(sel + kSelOn)) return;  // kernel-uniform: never repacked (the output is the posteriors)
@@ -1719,9 +1720,8 @@ static int side_stream(const qr_code *code, hipStream_t *out) {
 }
 
 // A repack decision point of the range starting at column f0 (full width h), on P.s (the variable
-// stream): the device
-// decides and, when it repacks, moves the columns (k_repack_rows) and updates the range's state
-// (k_repack_commit).
+// stream): one launch, k_repack_rows, decides and, when it repacks, moves the columns and (its
+// last workgroup) updates the range's state.
 static int launch_repack(const Plan &P, int f0, int h) {
     const qr_code *code = P.code;
     RepackArgs r;
@@ -1750,8 +1750,6 @@ static int launch_repack(const Plan &P, int f0, int h) {
     // at once (a few microseconds on the variable stream)
     k_repack_rows<<<(unsigned)std::min<int64_t>(rows, kRepackGrid), kRepackThreads, 0, P.s>>>(r);
     QR_LAUNCH_CHECK();
-    k_repack_commit<<<1, kCommitThreads, 0, P.s>>>(r);
-    QR_LAUNCH_CHECK();
     return QR_OK;
 }
 
@@ -1767,7 +1765,7 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
     hipEvent_t fork = code->ev[0], cA = code->ev[1], cB = code->ev[2], vA = code->ev[3], vB = code->ev[4];
     const int ld = P.ld, h = ld / 2;  // ld % 512 == 0: both ranges are h columns wide
     // Column repack (knob repack, default 1; needs the workspace's work set), decided on the device
-    // at every decision point (k_repack_rows / k_repack_commit before each variable sweep of a
+    // at every decision point (k_repack_rows before each variable sweep of a
     // range): the host enqueues the same launches whatever the data, never reads anything back
     // and never waits, so the decode is asynchronous and capturable (the host runs far ahead of
     // the GPU anyway: counts it could read without waiting would be an iteration-old at best).
