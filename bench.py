@@ -59,23 +59,24 @@ GUIDE_COPY_GBS = 6290.0  # float4 streaming copy measured on MI355X (MI355X_MICR
 # instruction occupies its SIMD 4 cycles, 32-bit VALU 2 cycles (MI355X_MICROARCH.md).
 SIMDS, CLOCK_HZ = 1024, 2.4e9
 # launches timed with hipEvents inside the timed region: the roofline's dominant kernel
-# (k_check<7> under the default schedule, k_fused<7> under split = 2) and the fused demap
-PRICED = ("check_d7", "fused_d7", "demap")
+# (k_check<7> under the default schedule, k_fused<7> under split = 2, k_resident<6> / k_iter<6> for
+# configs[1]'s small code) and the fused demap
+PRICED = ("check_d7", "fused_d7", "demap", "resident_d6", "iter_d6")
 
 # (name, workload, snr, batch, steps, BASELINE.json config it measures, launches timed with hipEvents
-#  inside its timed region, CPU leg)
+#  in its kernel-stats pass, the one its roofline prices (or None), CPU leg)
 SECONDARY = [
     ("configs1_reg1008_4pam", "reg1008_4pam", 3.0, 1024, 50, "configs[1]: reg-(3,6) N=1008, 4-PAM, B=1024",
-     ("resident_d6", "iter_d6"), False),
+     ("resident_d6", "iter_d6"), "resident_d6", False),
     ("configs3_dvbs2_16pam", "dvbs2_16pam", 13.0, 4096, 3,
      "configs[3]: N=64800 16-PAM, demap fused into the step, B=4096, 13 dB (all 50 iterations)",
-     ("check_d7", "demap"), True),
+     ("check_d7", "demap"), "demap", True),
     ("op_dvbs2_4pam_4.0dB", "dvbs2_4pam", 4.0, 4096, 3,
      "configs[2] code at its converging operating point 4.0 dB (frames stop early)",
-     ("check_d7", "repack"), False),
+     ("check_d7", "repack", "repack_out"), None, False),
     ("op_dvbs2_16pam_14.5dB", "dvbs2_16pam", 14.5, 4096, 3,
      "configs[3] at its converging operating point 14.5 dB (demap fused)",
-     ("check_d7", "repack", "demap"), False),
+     ("check_d7", "repack", "repack_out", "demap"), None, False),
 ]
 
 
@@ -120,6 +121,45 @@ def check_class_bytes(vid, cid, degree, B):
     return (16 * E_d + 8 * V_d + C_d) * B + B, dict(E=E_d, V=V_d, C=C_d)
 
 
+def resident_bytes(w):
+    """Algorithmic HBM bytes of one frame-resident decode (k_resident: messages and posteriors
+    live in LDS): LAPPRs and syndrome bits in, posteriors, success flag and iteration count out
+    per frame -- (16 V + C + 5) B."""
+    return (16 * w.V + w.C + 5) * w.B
+
+
+def demap_bytes(w):
+    """Algorithmic HBM bytes of one demap launch: n_hat (8 B) and x_hat (8 B) in per symbol, bps
+    LAPPRs (8 B each) out -- (16 + 8 bps) S B, S = V / bps symbols per frame."""
+    return (16 + 8 * w.bps) * (w.V // w.bps) * w.B
+
+
+def secondary_roofline(wl, w, ks, key, snr):
+    """The roofline of a secondary config's priced kernel: its algorithmic bytes over its hipEvent
+    launch time (HBM fraction) and its VALU issue fraction (PMC record of that config, at the clock
+    its launches run at: in-kernel stamps of an unprofiled clock pass)."""
+    if key not in ks:
+        return None
+    if key == "resident_d6":
+        bytes_launch, kname = resident_bytes(w), "k_resident<6> (frame-resident decode of the batch: one launch)"
+    elif key == "demap":
+        bytes_launch, kname = demap_bytes(w), f"k_demap_wave<{w.bps}> (wave-private soft demap of the batch)"
+    else:
+        return None
+    avg_s = ks[key]["avg_us"] / 1e6
+    ach = bytes_launch / avg_s / 1e9
+    t = pmc_entry(wl, w.B, key)
+    valu = None
+    if t and t.get("valu_insts_per_launch"):
+        valu = valu_fraction(t, avg_s, kernel_clock(wl, w.B, key, snr))
+    frac = ach / HBM_PEAK_GBS
+    return {"bound": "valu" if valu and valu["frac"] > frac else "hbm", "achieved": round(ach, 2),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(frac, 5),
+            "traffic": t.get("hbm_bytes_per_launch") if t else None, "kernel": kname,
+            "bytes_per_launch": int(bytes_launch), "avg_launch_us": round(avg_s * 1e6, 1),
+            "launches": ks[key]["launches"], "valu": valu}
+
+
 # ----------------------------------------------------------------- rank body
 def timed_region(step, sync, steps, warmup, before=None, after=None, device=None):
     """W untimed warmup steps, then EXACTLY K steps bracketed by a barrier + device
@@ -141,6 +181,7 @@ def timed_region(step, sync, steps, warmup, before=None, after=None, device=None
     sync()
     dist.barrier()
     elapsed = time.perf_counter() - t0
+    timed_region.local = elapsed  # this rank's own timed region (the per-rank record of N > 1)
     if after:
         after()
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -316,19 +357,22 @@ def probe_clock(w, n=16, ms=3.0):
         return None
 
 
-def kernel_clock(args):
-    """The shader clock the chip holds DURING the priced check launches, unprofiled: a child
-    process runs the same workload for a few steps on libqamr_clock.so, the diagnostic twin of
-    libqamr.so whose degree-7 check sweep stamps s_memtime / s_memrealtime around every
-    workgroup (decoder.hip QR_EXPERIMENT_CLOCK; MI355X_MICROARCH.md 'DVFS give-back' item 6).
-    Returns its JSON {"clock_ghz", "launch_us", "workgroups", "steps"} or None."""
+def kernel_clock(workload, batch, key="check_d7", snr=None):
+    """The shader clock the chip holds DURING the launches of profile key `key` (check_d7,
+    resident_d6 or demap), unprofiled: a child process runs the same workload for a few steps on
+    libqamr_clock.so, the diagnostic twin of libqamr.so whose degree-7 check sweep, frame-resident
+    decode and wave-private demapper stamp s_memtime / s_memrealtime around every workgroup
+    (QR_EXPERIMENT_CLOCK; MI355X_MICROARCH.md 'DVFS give-back' item 6).  Returns its JSON
+    {"clock_ghz", "launch_us", "workgroups", "steps"} or None."""
     import subprocess
 
     lib = os.path.join(ROOT, "qam-reconciliation_amd", "qamr", "libqamr_clock.so")
     if not os.path.exists(lib) or os.environ.get("QAMR_NO_CLOCK_PASS") == "1":  # (set under rocprofv3)
         return None
     cmd = [sys.executable, os.path.join(ROOT, "scripts", "diag", "clock_check.py"), "--json",
-           "--workload", args.workload, "--batch", str(args.batch)]
+           "--workload", workload, "--batch", str(batch), "--key", key]
+    if snr is not None:
+        cmd += ["--snr", str(snr)]
     try:
         r = subprocess.run(cmd, env=dict(os.environ, QAMR_LIB=lib), capture_output=True, text=True, timeout=240)
         d = json.loads(r.stdout.strip().splitlines()[-1])
@@ -337,8 +381,52 @@ def kernel_clock(args):
         return None
 
 
+def pmc_entry(workload, batch, key):
+    """The PMC record (rocprofv3 --pmc passes, scripts/summarize_profile.py) of the launches of
+    `key` in `workload` at `batch` frames: profiles/pmc_traffic.json (the headline's dominant
+    kernel) or an entry of profiles/pmc_secondary.json (the secondary configs' priced kernels)."""
+    recs = []
+    for name in ("pmc_traffic.json", "pmc_secondary.json"):
+        try:
+            d = json.load(open(os.path.join(ROOT, "profiles", name)))
+            recs += d if isinstance(d, list) else [d]
+        except Exception:
+            pass
+    for t in recs:
+        if t.get("workload") == workload and int(t.get("batch", -1)) == batch and t.get("kernel_key") == key \
+                and t.get("math", 0) == 0:
+            return t
+    return None
+
+
+def valu_fraction(t, avg_s, clk_kernel=None, clk_live=None):
+    """SIMD issue time of a launch's VALU instructions (4 cycles per wave64 instruction -- fp64 or
+    32-bit: SQ_ACTIVE_INST_VALU == SQ_INSTS_VALU in these kernels -- counts from the PMC record t)
+    at the shader clock the launches run at, over the live launch time avg_s."""
+    n_all, n64 = t["valu_insts_per_launch"], t.get("valu_f64_insts_per_launch", 0)
+    clk_pmc = t.get("clock_ghz_pmc")
+    clk_ghz = clk_kernel["clock_ghz"] if clk_kernel else None
+    clk = clk_ghz or clk_live or clk_pmc or CLOCK_HZ / 1e9
+    busy = 4 * n_all / SIMDS / (clk * 1e9)  # s of SIMD issue time
+    return {"wave_insts_per_launch": int(n_all), "f64_wave_insts_per_launch": int(n64),
+            "clock_ghz": round(clk, 3),
+            "clock_source": "in-kernel stamps of the priced launches (libqamr_clock.so, unprofiled, same workload)"
+            if clk_ghz else "live (qr_clock_probe beside an unprofiled step)" if clk_live
+            else "profiled PMC pass" if clk_pmc else "spec",
+            "clock_pass": clk_kernel,
+            "clock_ghz_pmc": round(clk_pmc, 3) if clk_pmc else None,
+            "issue_ms": round(busy * 1e3, 3),
+            "frac": round(busy / avg_s, 4),
+            "busy_pmc": round(t["valu_busy_pmc"], 4) if t.get("valu_busy_pmc") else None,
+            "source": t.get("source"),
+            "note": "SIMD issue time of the launch's VALU instructions (4 cycles per wave64 instruction, counts "
+                    "from the rocprofv3 --pmc record) at the shader clock named by clock_source, over the live "
+                    "launch time; clock_ghz_pmc = GRBM_GUI_ACTIVE per XCD / launch time of the profiled pass; "
+                    "busy_pmc = rocprofv3 VALUBusy of the profiled launch"}
+
+
 KERNEL_KEYS = ("check", "check_d7", "check_d6", "check1", "fused_d7", "var", "var_init", "parity", "status", "demap",
-               "iter_d6", "resident_d6", "repack")
+               "iter_d6", "resident_d6", "repack", "repack_out")
 
 
 def kernel_stats(keys=KERNEL_KEYS):
@@ -382,48 +470,22 @@ def roofline(args, w, kstats, dev, world=1):
             bytes_launch, _ = check_class_bytes(w.vid, w.cid, 7, B)
             kname = "k_check<7,Normal> (degree-7 check-node sweep)"
         kkey = "check_d7"
+    elif "resident_d6" in kstats:
+        bytes_launch, kname = resident_bytes(w), "k_resident<6> (frame-resident decode: one launch per decode)"
+        kkey = "resident_d6"
     else:
         return None
     avg_s = kstats[kkey]["avg_us"] / 1e6
     ach = bytes_launch / avg_s / 1e9
     traffic, valu = None, None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        try:
-            t = json.load(open(pmc))
-            if t.get("workload") == args.workload and int(t.get("batch", -1)) == B \
-                    and t.get("kernel_key") == kkey and t.get("math", 0) == 0:
-                traffic = t.get("hbm_bytes_per_launch")
-                if t.get("valu_insts_per_launch"):
-                    n_all, n64 = t["valu_insts_per_launch"], t.get("valu_f64_insts_per_launch", 0)
-                    # every wave64 VALU instruction (fp64 or 32-bit) holds its SIMD for one
-                    # quad-cycle in this kernel (SQ_ACTIVE_INST_VALU == SQ_INSTS_VALU)
-                    clk_pmc = t.get("clock_ghz_pmc")
-                    kc = kernel_clock(args) if (world == 1 and kkey == "check_d7") else None
-                    clk_kernel = kc["clock_ghz"] if kc else None
-                    clk_live = None if clk_kernel else probe_clock(w)
-                    clk = clk_kernel or clk_live or clk_pmc or CLOCK_HZ / 1e9
-                    busy = 4 * n_all / SIMDS / (clk * 1e9)  # s of SIMD issue time
-                    valu = {"wave_insts_per_launch": int(n_all), "f64_wave_insts_per_launch": int(n64),
-                            "clock_ghz": round(clk, 3),
-                            "clock_source": "in-kernel stamps of the check launches (libqamr_clock.so, "
-                                            "unprofiled, same workload)" if clk_kernel
-                            else "live (qr_clock_probe beside an unprofiled step)" if clk_live
-                            else "profiled PMC pass" if clk_pmc else "spec",
-                            "clock_pass": kc,
-                            "clock_ghz_probe_min_max": getattr(probe_clock, "spread", None) if clk_live else None,
-                            "clock_ghz_pmc": round(clk_pmc, 3) if clk_pmc else None,
-                            "issue_ms": round(busy * 1e3, 3),
-                            "frac": round(busy / avg_s, 4),
-                            "busy_pmc": round(t["valu_busy_pmc"], 4) if t.get("valu_busy_pmc") else None,
-                            "source": t.get("source"),
-                            "note": "SIMD issue time of the launch's VALU instructions (4 cycles per wave64 "
-                                    "instruction, counts from profiles/pmc_traffic.json, rocprofv3 --pmc) at the "
-                                    "shader clock named by clock_source, over the live launch time; "
-                                    "clock_ghz_pmc = GRBM_GUI_ACTIVE per XCD / launch time of the profiled pass; "
-                                    "busy_pmc = rocprofv3 VALUBusy of the profiled launch"}
-        except Exception:
-            traffic = None
+    t = pmc_entry(args.workload, B, kkey)
+    if t:
+        traffic = t.get("hbm_bytes_per_launch")
+        if t.get("valu_insts_per_launch"):
+            kc = kernel_clock(args.workload, B, kkey, args.snr) if (world == 1 and kkey in ("check_d7", "resident_d6")) \
+                else None
+            clk_live = None if kc else probe_clock(w)
+            valu = valu_fraction(t, avg_s, kc, clk_live)
     copy_gbps = copy_bandwidth(dev)
     frac = ach / HBM_PEAK_GBS
     bound = "valu" if valu and valu["frac"] > frac else "hbm"
@@ -437,29 +499,41 @@ def roofline(args, w, kstats, dev, world=1):
 
 def secondary(args, rank, local):
     """configs[1], configs[3] and the converging operating points, each on its own
-    resident batch, timed separately from the headline (same step definition).  Each carries
-    the hipEvent-timed average of its dominant launches (recorded on their launch streams inside
-    its timed region) so a kernel trace of the same config can be reconciled with its step; the
-    configs[3] line also carries its CPU baseline (demap + decode on the host cores, SURVEY.md
-    8(d)'s demap leg)."""
+    resident batch, timed separately from the headline (same step definition, no profiling in the
+    timed region).  A second, untimed pass of as many steps records the hipEvent-timed average of
+    its dominant launches (on their launch streams) so a kernel trace of the same config can be
+    reconciled with its step; configs[1] and configs[3] carry a roofline of their priced kernel
+    (k_resident<6>; the 16-PAM demapper), and the configs[3] line its CPU baseline (demap + decode
+    on the host cores, SURVEY.md 8(d)'s demap leg)."""
     import types
 
     import qamr
     import torch
 
     out = {}
-    for name, wl, snr, batch, steps, what, keys, cpu_leg in SECONDARY:
+    for name, wl, snr, batch, steps, what, keys, priced, cpu_leg in SECONDARY:
         w = Work(wl, snr, batch, args.max_iter, args.alpha, args.seed, rank, local)
-
-        def before(keys=keys):
-            qamr.profile_reset()
-            qamr.profile_select(keys)
-            qamr.profile_enable(True)
-
-        el = timed_region(w.step, w.sync, steps, 1, before, lambda: qamr.profile_enable(False), device=w.dev)
+        el = timed_region(w.step, w.sync, steps, 1, device=w.dev)
+        mean_it = round(w.mean_iterations(), 3)
+        # kernel-stats pass (untimed): the same steps with events around the selected launches
+        qamr.profile_reset()
+        qamr.profile_select(keys)
+        qamr.profile_enable(True)
+        for _ in range(steps):
+            w.step()
+        w.sync()
+        qamr.profile_enable(False)
+        ks = kernel_stats(keys)
+        if "repack" in ks:  # the device's repack count of the last decode: most decision points move nothing
+            (r0, r1), (w0, w1) = w.dec.repack_stats(w.batch.ld, args.max_iter)
+            ks["repack"].update(repacks_per_decode=r0 + r1, final_widths=[w0, w1],
+                                note="k_repack_rows: every decision point (one before each variable sweep); "
+                                     "only repacks_per_decode of them move columns")
         out[name] = {"frames_per_s": round(w.B * steps / el, 1), "ms_per_step": round(1e3 * el / steps, 3),
-                     "steps": steps, "batch": w.B, "snr_db": w.snr, "mean_iterations": round(w.mean_iterations(), 3),
-                     "what": what, "kernels": kernel_stats(keys)}
+                     "steps": steps, "batch": w.B, "snr_db": w.snr, "mean_iterations": mean_it,
+                     "what": what, "kernels": ks}
+        if priced:
+            out[name]["roofline"] = secondary_roofline(wl, w, ks, priced, snr)
         if cpu_leg and args.cpu_seconds > 0:
             out[name]["cpu_baseline"] = cpu_baseline(types.SimpleNamespace(workload=wl, max_iter=args.max_iter), w,
                                                      args.cpu_seconds)
@@ -594,8 +668,18 @@ def main(argv=None):
             qamr.profile_enable(False)
 
     elapsed = timed_region(w.step, w.sync, args.steps, args.warmup, before, after, device=w.dev)
+    local_elapsed = timed_region.local
     counters = w.counters()
     dist.all_reduce_sum(counters)
+    kstats = kernel_stats() if prof else {}
+    # every rank's own timed region and its priced kernel's hipEvent average, gathered on rank 0
+    # (N > 1: a slow rank, an imbalance or a slow barrier shows beside the max-reduced value)
+    pkey = next((k for k in PRICED if k in kstats and k != "demap"), None)
+    per = torch.zeros(2 * world, dtype=torch.float64, device=w.dev)
+    per[rank] = 1e3 * local_elapsed / args.steps
+    per[world + rank] = kstats[pkey]["avg_us"] if pkey else -1.0
+    dist.all_reduce_sum(per)
+    per = per.cpu().numpy()
     # the GPU each rank bound (LOCAL_RANK, or QAMR_BENCH_DEVICE in a rehearsal), gathered on rank 0
     bound = torch.zeros(world, dtype=torch.int64, device=w.dev)
     bound[rank] = 1 + (w.local if stub else torch.cuda.current_device())
@@ -617,7 +701,6 @@ def main(argv=None):
     else:
         from qamr.pipeline import SofteningPipeline
 
-        kstats = kernel_stats() if prof else {}
         roof = roofline(args, w, kstats, w.dev, world) if (prof and rank == 0) else None
         it_mean = w.mean_iterations()
         # whole-decode algorithmic bandwidth (SURVEY.md 8(d) B_frame at the iterations actually run)
@@ -645,6 +728,12 @@ def main(argv=None):
         if world == 1 and not args.no_secondary:
             w.free()
             out["secondary"] = secondary(args, rank, local)
+    if world > 1:
+        out["per_rank"] = {"ms_per_step": [round(float(v), 3) for v in per[:world]],
+                           "priced_kernel": pkey,
+                           "avg_launch_us": [round(float(v), 1) if v >= 0 else None for v in per[world:]],
+                           "note": "each rank's own timed region (the line's ms_per_step is their max) and the "
+                                   "hipEvent average of its priced launches"}
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.finalize()

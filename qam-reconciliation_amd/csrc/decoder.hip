@@ -39,6 +39,45 @@ namespace qr {
 
 enum CheckMode { kFirst = 0, kNormal = 1, kParityOnly = 2 };
 
+// Device-side index checks of the debug build (make -C csrc DEBUG=1 -> qamr/libqamr_debug.so,
+// QR_DEBUG_ASSERT=1; SURVEY.md 5 -- the reference turns bounds checks off, decoder.pyx:181,240,
+// 289,332,399,411): QR_DCHECK(ok, site, a, b) counts every failed check in g_dbg and keeps the
+// first failure's site and two values; the first failing lane also prints them.  Non-fatal (no
+// trap): the test reads the counts through qr_debug_asserts (tests/test_gpu_debug_build.py).  The
+// product library compiles every check away.
+#ifndef QR_DEBUG_ASSERT
+#define QR_DEBUG_ASSERT 0
+#endif
+#if QR_DEBUG_ASSERT
+__device__ unsigned long long g_dbg[4];  // {failed checks, first site, first a, first b}
+__device__ __noinline__ void dcheck_fail(int site, long long a, long long b) {
+    if (atomicAdd(&g_dbg[0], 1ull) == 0ull) {
+        g_dbg[1] = (unsigned long long)site;
+        g_dbg[2] = (unsigned long long)a;
+        g_dbg[3] = (unsigned long long)b;
+        printf("qamr debug check %d failed: a=%lld b=%lld (block %u thread %u)\n", site, a, b, blockIdx.x, threadIdx.x);
+    }
+}
+#define QR_DCHECK(ok, site, a, b)                                   \
+    do {                                                            \
+        if (!(ok)) dcheck_fail((site), (long long)(a), (long long)(b)); \
+    } while (0)
+#else
+#define QR_DCHECK(ok, site, a, b) ((void)0)
+#endif
+// check sites (qr_debug_asserts reports the first failure's site)
+enum DebugSite {
+    kDbgLaneFrame = 1,     // lane_frame: a listed column outside the sweep's range
+    kDbgNarrowFrame = 2,   // narrow sweeps: lane frame outside the repacked range's first 64 columns
+    kDbgNarrowNode = 3,    // narrow sweeps: check id / CSR offset out of range
+    kDbgRepackList = 4,    // k_repack_rows: list entry not ascending or outside [f0, f0 + w)
+    kDbgRepackSlot = 5,    // gather_rows: a slot's byte offset outside its row group
+    kDbgRepackFid = 6,     // hand-out / commit / k_repack_output: frame id outside [0, ld)
+    kDbgCompact = 7,       // k_compact: list index outside the range
+    kDbgResPost = 8,       // k_resident: posterior index outside [0, V)
+    kDbgResMsg = 9,        // k_resident: LDS message index outside [0, C D)
+};
+
 // Check-node arithmetic: the reference's box-plus bit for bit -- glibc exp/log restated
 // (glibc_math.hpp, the box-plus part of its tables, 8 KiB, staged in LDS per workgroup; a few
 // constants pinned in VGPRs, GlibcK) -- so every message, posterior and output LAPPR is
@@ -134,11 +173,13 @@ struct CheckArgs {
     unsigned nmain;
     int per_t;
     // Column repack (run_split2): sel -> the range's RangeSel, or null.  Once the device has
-    // repacked the range (sel[kSelOn]) its posteriors and syndrome bits live in the work set
-    // (post_w, synd_w).
+    // repacked the range (sel[kSelOn]) its posteriors live in the work set (post_w) and its
+    // messages and syndrome bits in the work set's column set sel[kSelBuf] (c2v / c2v_alt,
+    // synd_w[0] / synd_w[1]).
     const int32_t *sel;
     const double *post_w;
-    const uint8_t *synd_w;
+    const uint8_t *synd_w[2];
+    double *c2v_alt;
 };
 
 // One variable sweep over the frame columns [f_off, f_off + ny*ft).
@@ -160,28 +201,35 @@ struct VarArgs {
     int32_t *finite;
     double fin_bound;
     int fin_B;
-    const int32_t *sel;  // as CheckArgs: the range's RangeSel or null; work-set LAPPRs / posteriors
-    const double *lappr_w;
+    const int32_t *sel;  // as CheckArgs: the range's RangeSel or null; work-set LAPPRs / posteriors / messages
+    const double *lappr_w[2];
     double *post_w;
+    const double *c2v_alt;
 };
 
 // The state of one frame range of the two-stream schedule, in device memory (the workspace's
 // count block), read by every launch of that range and written only by a repack's commit (k_repack_rows): whether
 // the range has moved to the repack work set, its width there (its running frames occupy the
-// first columns), and how many repacks it went through.
-enum RangeSelField { kSelOn = 0, kSelW = 1, kSelRepacks = 2, kSelArrive = 3, kSelInts = 4 };
+// first columns), how many repacks it went through, and which of the work set's two column sets
+// (messages, LAPPRs, syndrome bits) holds it: a repack gathers the running columns of one set
+// into the other, so no column is overwritten while another thread may still read it.
+enum RangeSelField { kSelOn = 0, kSelW = 1, kSelRepacks = 2, kSelArrive = 3, kSelBuf = 4, kSelInts = 5 };
 
 // Kernel-uniform: the arrays a range's launch reads once the device has repacked the range.
 __device__ __forceinline__ void select_range(CheckArgs &a) {
     if (a.sel && sld(a.sel + kSelOn)) {
+        const int b = sld(a.sel + kSelBuf);
         a.post = a.post_w;
-        a.synd = a.synd_w;
+        a.synd = b ? a.synd_w[1] : a.synd_w[0];  // (selects: a dynamic index would put a in scratch)
+        if (b) a.c2v = a.c2v_alt;
     }
 }
 __device__ __forceinline__ void select_range(VarArgs &a) {
     if (a.sel && sld(a.sel + kSelOn)) {
-        a.lappr = a.lappr_w;
+        const int b = sld(a.sel + kSelBuf);
+        a.lappr = b ? a.lappr_w[1] : a.lappr_w[0];
         a.post = a.post_w;
+        if (b) a.c2v = a.c2v_alt;
     }
 }
 
@@ -200,7 +248,9 @@ __device__ __forceinline__ int lane_frame(const int32_t *alist, const int32_t *a
     if (!alist) return f_off + p;
     const int cnt = *acount;
     live = p < cnt;
-    return alist[f_off + (live ? p : cnt - 1)];
+    const int f = alist[f_off + (live ? p : cnt - 1)];
+    QR_DCHECK(f >= f_off + (live ? p : cnt - 1), kDbgLaneFrame, f, f_off + p);  // ascending, in the range
+    return f;
 }
 
 
@@ -229,6 +279,13 @@ struct CheckIn {
         for (int i = 0; i < D; ++i) c[i] = ld_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), a.ld), b8, a.ld);
     }
 };
+
+// The syndrome sign of a check's outputs (decoder.pyx:360-369: s * message, s = -1 when the
+// syndrome bit is set): s * x with s = +-1 only flips x's sign bit (for NaN too, as the compiled
+// multiply by the selected constant did), so it is one XOR of the high word with a per-check mask
+// instead of the compiler's XOR + select per output.
+__device__ __forceinline__ uint32_t sign_mask(uint8_t sb) { return sb ? 0x80000000u : 0u; }
+__device__ __forceinline__ double apply_sign(double x, uint32_t smask) { return g_make(g_hi(x) ^ smask, g_lo(x)); }
 
 // Degrees whose round loop the compiler still unrolls fully (above, the packed update's
 // register arrays would be indexed dynamically, i.e. live in scratch): the unpacked strict
@@ -262,9 +319,10 @@ __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m
         double out[D];
         double *wb = hb + (threadIdx.x >> 6) * kPackWaveDoubles;
         check_strict_packed<D, FIN ? kClampFinite : kClampFull>(m, out, wb, tab, K);
+        const uint32_t smask = sign_mask(sb);
 #pragma unroll
         for (int i = 0; i < D; ++i)
-            if (live) st_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), ld), b8, ld, s * out[i]);
+            if (live) st_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), ld), b8, ld, apply_sign(out[i], smask));
         return;
     }
     double F[D - 1];
@@ -407,6 +465,8 @@ __device__ __forceinline__ void check_narrow(const CheckArgs &a, uint32_t task, 
     const bool valid = ci < a.n_checks;
     const int cc = a.checks[valid ? ci : a.n_checks - 1];
     int base = a.chk_ptr[cc];
+    QR_DCHECK(f >= a.f_off && f < a.f_off + kNarrowW, kDbgNarrowFrame, f, a.f_off);
+    QR_DCHECK(cc >= 0 && base >= 0 && a.chk_ptr[cc + 1] - base == D, kDbgNarrowNode, cc, base);
     const size_t ld = a.ld;
     const uint8_t sb = a.synd[(size_t)cc * ld + f];
     uint32_t par = sb;
@@ -452,6 +512,7 @@ __device__ __forceinline__ void var_narrow_sweep(const VarArgs &a) {
         const int f = lane_frame(a.alist, a.acount, a.f_off, grp * kNarrowFrames + (int)(threadIdx.x % kNarrowFrames), live);
         const int64_t v = (int64_t)(t >> lg) * kNarrowNodes + threadIdx.x / kNarrowFrames;
         if (!live || v >= a.V || !a.active[f]) continue;
+        QR_DCHECK(f >= a.f_off && f < a.f_off + kNarrowW, kDbgNarrowFrame, f, a.f_off);
         double p = a.lappr[(size_t)v * ld + f];
         const int b = a.var_ptr[v], e = a.var_ptr[v + 1];
         for (int k = b; k < e; ++k) p += a.c2v[(size_t)a.var_edge[k] * ld + f];  // decoder.pyx:292-293
@@ -460,41 +521,15 @@ __device__ __forceinline__ void var_narrow_sweep(const VarArgs &a) {
 }
 
 // QR_EXPERIMENT_CLOCK (diagnostic builds only, scripts/diag/clock_check.py): every workgroup of
-// the degree-7 main-loop check sweep stamps the shader clock (s_memtime) and the 100 MHz
-// realtime counter around its work and adds both spans to g_clk (vector atomics); the effective
-// clock of the unprofiled launch is sum(cycles) / sum(ticks) x 100 MHz (MI355X_MICROARCH.md
-// 'DVFS give-back' item 6).  qr_debug_clock reads and clears the sums.
-#ifndef QR_EXPERIMENT_CLOCK
-#define QR_EXPERIMENT_CLOCK 0
-#endif
+// the degree-7 main-loop check sweep and of the frame-resident decode stamps the shader clock
+// (ClkScope, qamr_internal.hpp) around its work and adds its spans to g_clk; the effective clock of
+// the unprofiled launch is sum(cycles) / sum(ticks) x 100 MHz (MI355X_MICROARCH.md 'DVFS give-back'
+// item 6).  qr_debug_clock reads and clears the sums.
 #if QR_EXPERIMENT_CLOCK
 __device__ unsigned long long g_clk[3];
 // realtime start / end of every workgroup of the last such launch (up to kWgTimes workgroups):
 // the launch's occupancy over time, i.e. how much of it is the drain at its end
-constexpr int kWgTimes = 1 << 16;
 __device__ unsigned long long g_wgt[2 * kWgTimes];
-struct ClkScope {
-    bool on;
-    uint64_t c0, r0;
-    __device__ explicit ClkScope(bool on_) : on(on_) {
-        c0 = __builtin_amdgcn_s_memtime();
-        r0 = __builtin_amdgcn_s_memrealtime();
-    }
-    __device__ ~ClkScope() {
-        __syncthreads();
-        if (on && threadIdx.x == 0) {
-            const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-            atomicAdd(&g_clk[0], (unsigned long long)(c1 - c0));
-            atomicAdd(&g_clk[1], (unsigned long long)(r1 - r0));
-            atomicAdd(&g_clk[2], 1ull);
-            const unsigned b = blockIdx.y * gridDim.x + blockIdx.x;
-            if (b < (unsigned)kWgTimes) {
-                g_wgt[2 * b] = r0;
-                g_wgt[2 * b + 1] = r1;
-            }
-        }
-    }
-};
 #endif
 template <int D, int MODE, bool NT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))) k_check(CheckArgs a) {
@@ -521,7 +556,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
     }
     if (!frames_block_live(a.acount, by, a.g.lft)) return;  // block-uniform
 #if QR_EXPERIMENT_CLOCK
-    ClkScope clk(D == 7 && MODE == kNormal);
+    ClkScope clk(D == 7 && MODE == kNormal, g_clk, g_wgt);
 #endif
     if (MODE != kParityOnly) stage_glibc_tables(&tab, a.gglibc);
     if constexpr (MODE != kParityOnly && kPacked<D>) {
@@ -703,6 +738,8 @@ struct ResArgs {
     const GlibcTables *gglibc;
     double fin_bound;  // |lappr| below it for every variable -> the finite clamp (0: never)
     int dv;            // every variable of degree dv <= 3 and E < 2^16 (0: otherwise)
+    int32_t *rsel;     // the workspace's RangeSel block: reset to "never repacked" (repack stats)
+    int w0, w1;        // its initial widths
 };
 
 // parity of the posteriors in LDS (decoder.pyx:235-257): 1 iff some check of this thread fails
@@ -766,6 +803,8 @@ __device__ __forceinline__ void resident_loop(const ResArgs &a, int f, double *m
             double m[D];
 #pragma unroll
             for (int i = 0; i < D; ++i) {
+                QR_DCHECK(a.chk_var[cc * D + i] >= 0 && a.chk_var[cc * D + i] < a.V, kDbgResPost, cc, a.chk_var[cc * D + i]);
+                QR_DCHECK(i * a.C + cc < a.C * D, kDbgResMsg, cc, i);
                 const double p = post[a.chk_var[cc * D + i]];
                 par ^= (p < 0.0) ? 1u : 0u;     // decoder.pyx:243-246
                 m[i] = p - msg[i * a.C + cc];    // :296-297
@@ -773,10 +812,10 @@ __device__ __forceinline__ void resident_loop(const ResArgs &a, int f, double *m
             if (live) bad |= (par == 1u) ? 1u : 0u;
             double out[D];
             check_strict_packed<D, FIN ? kClampFinite : kClampFull>(m, out, wb, tab, K);
-            const double s = sb ? -1.0 : 1.0;
+            const uint32_t smask = sign_mask(sb);
             if (live) {
 #pragma unroll
-                for (int i = 0; i < D; ++i) msg[i * a.C + cc] = s * out[i];  // only this lane reads them back
+                for (int i = 0; i < D; ++i) msg[i * a.C + cc] = apply_sign(out[i], smask);  // only this lane reads them back
             }
         }
         // the parity of post(t-1) (t = 1: post(0), whose parity is the input's, already tested)
@@ -792,6 +831,8 @@ __device__ __forceinline__ void resident_loop(const ResArgs &a, int f, double *m
 #pragma unroll
             for (int q = 0; q < 3; ++q) {
                 if (q < dv) {
+                    QR_DCHECK((vm[q] & 0xFFFFu) < (uint32_t)(a.C * D) && (vm[q] >> 16) < (uint32_t)(a.C * D), kDbgResMsg,
+                              vm[q] & 0xFFFFu, vm[q] >> 16);
                     const double m0 = msg[vm[q] & 0xFFFFu], m1 = msg[vm[q] >> 16];
                     p0 += m0;
                     p1 += m1;
@@ -811,6 +852,8 @@ __device__ __forceinline__ void resident_loop(const ResArgs &a, int f, double *m
             const int n = max(e0 - b0, e1 - b1);
             for (int q = 0; q < n; ++q) {
                 const bool h0 = b0 + q < e0, h1 = b1 + q < e1;
+                QR_DCHECK(a.var_msg[h0 ? b0 + q : 0] < a.C * D && a.var_msg[h1 ? b1 + q : 0] < a.C * D, kDbgResMsg,
+                          a.var_msg[h0 ? b0 + q : 0], a.var_msg[h1 ? b1 + q : 0]);
                 const double m0 = msg[a.var_msg[h0 ? b0 + q : 0]];  // (edge 0: an in-bounds dummy)
                 const double m1 = msg[a.var_msg[h1 ? b1 + q : 0]];
                 if (h0) p0 += m0;
@@ -830,8 +873,14 @@ __global__ void __launch_bounds__(kResThreads) __attribute__((amdgpu_waves_per_e
     extern __shared__ double res_dyn[];
     __shared__ GlibcTablesBP tab;
     __shared__ double hb[(kResThreads / 64) * kPackWaveDoubles];
+#if QR_EXPERIMENT_CLOCK
+    ClkScope clk(true, g_clk, nullptr);  // every exit below is block-uniform
+#endif
     const int q = (a.B + 7) / 8;
     const int f = (int)(blockIdx.x & 7u) * q + (int)(blockIdx.x >> 3);
+    // qr_decode_repack_stats after a frame-resident decode: 0 repacks, widths ld/2 (no extra launch)
+    if (blockIdx.x == 0 && threadIdx.x < 2 * kSelInts)
+        a.rsel[threadIdx.x] = (threadIdx.x % kSelInts == kSelW) ? (threadIdx.x < kSelInts ? a.w0 : a.w1) : 0;
     if (f >= a.B) return;  // block-uniform
     stage_glibc_tables(&tab, a.gglibc);
     const int tid = threadIdx.x;
@@ -1038,6 +1087,7 @@ __global__ void __launch_bounds__(1024) k_compact(int f0, int f1, uint8_t *__res
             off += i < w ? wsum[i] : 0;
             tot += wsum[i];
         }
+        QR_DCHECK(!a || off + __popcll(m & ((1ull << lane) - 1ull)) <= f - f0, kDbgCompact, off, f - f0);
         if (a) list[f0 + off + __popcll(m & ((1ull << lane) - 1ull))] = f;
         base += tot;
         __syncthreads();  // wsum is rewritten by the next chunk
@@ -1057,35 +1107,40 @@ __global__ void __launch_bounds__(1024) k_compact(int f0, int f1, uint8_t *__res
 //
 // Everything is decided on the device, so the decode stays asynchronous and capturable: at
 // each decision point (before a range's variable sweep, on the variable stream) k_repack_rows
-// reads the range's running-frame count (written by its last status launch) and its RangeSel; when the running frames fill at most pct % of the range's width w,
-// the range moves to w' = max(64, count rounded up to 64):
-//   * messages: compacted in place in the workspace's c2v rows (the range's own columns);
-//   * posteriors, LAPPRs, syndrome bits: the first repack gathers them from the caller's arrays
-//     into the repack work set (same ld, the range's own columns), later ones compact them in
-//     place there; frames stopped since the last repack first hand their posteriors (in the
-//     work set) to the caller's output through fid;
+// reads the range's running-frame count (written by its last status launch) and its RangeSel;
+// when the running frames fill at most pct % of the range's width w, the range moves to
+// w' = max(64, count rounded up to 64):
+//   * messages, LAPPRs, syndrome bits: gathered from the range's current column set into the
+//     other one of the work set's two (set 0: the workspace's c2v rows + lappr_w[0] / synd_w[0],
+//     set 1: c2v_alt + lappr_w[1] / synd_w[1]; the first repack reads the caller's LAPPRs and
+//     syndrome bits and the workspace's messages, and writes set 1).  Source and destination
+//     never alias, so the moves need no ordering between threads: no barrier, any grid, every
+//     load of a thread in flight at once -- the row moves run at copy bandwidth (round 5
+//     compacted in place, one barrier per row chunk: 2-3 ms per repack, latency-bound);
+//   * posteriors are not moved (the variable sweep right after writes every running frame's
+//     posterior in its new column, in the work set's post rows); frames stopped since the last
+//     repack first hand theirs to the caller's output through fid (again barrier-free:
+//     work set -> output);
 //   * fid[column] = the frame the column holds (-1: none), the list becomes the identity, the
 //     active flags follow the frames.
-// In-place compaction of a row (list ascending, so a column is only ever moved to a column at or
-// before it): chunks of columns in ascending order, all reads of a chunk complete before any of
-// its writes (one barrier); a later chunk reads only columns beyond every column written before.
 // The decision points run on the variable stream beside the other range's check launch, whose
 // waves hold 4 x 120 of the 512 VGPRs of a SIMD: the repack waves must fit in the 32 left, or
 // their workgroups are dispatched only as check workgroups retire (a first 48-VGPR version waited
-// ~0.26 ms per decision point at 4-PAM 4.0 dB).  So the chunk's slots (source and destination
-// element offsets) are computed once and held in registers for all of a workgroup's rows, and
-// loads and stores are raw buffer accesses off a scalar base.
+// ~0.26 ms per decision point at 4-PAM 4.0 dB).  So each thread's slots (source and destination
+// element offsets of a group of rows) are computed once and held in registers for all the row
+// groups it moves, and loads and stores are raw buffer accesses off a scalar base.
 // Register note (MI355X, measured, mechanism not established): the kernels launched beside the
 // check waves (120 VGPRs allocated, 4 per SIMD) must allocate 16 or 32 VGPRs, not 24.  With this
 // kernel at 24 (22 used) every dense iteration ran slower, although at a dense iteration it only
 // reads two words and exits: headline 9 547 vs 9 790 frames/s (same box, alternating runs), 9 798
 // with the round's earlier 28-VGPR version; a variable sweep at 24 (18 used) cost the same
 // (9 552 vs 9 776).  So k_repack_rows allocates 32 (an empty asm clobbering v31) and k_var stays
-// at 16 (32-bit task arithmetic in its narrow sweep).
+// at 16 (32-bit task arithmetic in its narrow sweep); tests/test_vgpr_budget.py checks both in the
+// built code object.
 constexpr int kRepackThreads = 256;
 constexpr int kRepackPer = 4;  // slots per thread per chunk
 constexpr int kRepackChunk = kRepackThreads * kRepackPer;
-constexpr int kRepackGrid = 512;  // workgroups of k_repack_rows (2 per CU)
+// workgroups of k_repack_rows: knob repack_grid (default 512, 2 per CU)
 
 struct RepackArgs {
     int f0, h, ld, pct;  // the range's first column and full width; repack threshold (percent)
@@ -1094,17 +1149,17 @@ struct RepackArgs {
     int32_t *sel;          // its RangeSel
     int32_t *list;         // active-frame list (absolute columns, list[f0 + p])
     uint8_t *active;
-    double *c2v;
+    double *c2v[2];              // message rows of column sets 0 (the workspace's) and 1
     double *out_post;            // the caller's posterior output (frame f at column f)
     const double *lappr_in;      // the caller's LAPPRs
     const uint8_t *synd_in;      // the caller's syndrome bits
-    double *post_w, *lappr_w;    // the work set
-    uint8_t *synd_w;
+    double *post_w;              // the work set's posteriors
+    double *lappr_w[2];          // its LAPPRs and syndrome bits, column sets 0 and 1
+    uint8_t *synd_w[2];
     int32_t *fid_w;
 };
 
-// The decision, taken identically by every workgroup of k_repack_rows
-// (their inputs do not change between the two launches).
+// The decision, taken identically by every workgroup of k_repack_rows.
 __device__ __forceinline__ bool repack_go(const RepackArgs &r, int &cnt, int &w, int &w_new) {
     cnt = sld(r.count);
     w = sld(r.sel + kSelW);
@@ -1140,38 +1195,43 @@ __device__ __forceinline__ void rb_store(__amdgpu_buffer_rsrc_t r, uint32_t off,
     __builtin_amdgcn_raw_buffer_store_b8(v, r, off, 0, 0);
 }
 
-// One chunk of one array's rows for this workgroup, which owns the contiguous rows [ra, rb) of it.
-// The chunk's slots (u, tid) -> (row j of a group of rg consecutive rows, column p0 + q): element
-// (row, f0 + p0 + q) <- (row, list[f0 + p0 + q]); groups of rg rows (rg > 1 when the count is small,
-// so a barrier moves several short rows), one group per barrier.  src_el / dst_el: the slots'
-// byte offsets inside a group of double rows (8 (j ld + column)), kRepackNone for an empty slot.
+// Gather the columns of this thread's slots from rows [0, n) of src into dst, row groups of rg
+// rows walked grid-stride by the workgroups: slot u of a group = (row j < rg of the group, one
+// column); src_el / dst_el: its byte offsets inside a group of double rows (8 (j ld + column)),
+// kRepackNone for an empty slot (a byte row group shifts them right by 3; an empty slot's offset
+// stays past the group either way).  src and dst never alias (two column sets, or work set ->
+// output), so there is no ordering to keep.
 constexpr uint32_t kRepackNone = 0xFFFFFFF0u;  // past any group: loads 0, stores nothing
-template <typename T>
-__device__ __forceinline__ void compact_rows(const T *src, T *dst, int64_t ra, int64_t rb, int ld, int rg,
-                                             const uint32_t (&src_el)[kRepackPer],
-                                             const uint32_t (&dst_el)[kRepackPer]) {
-    for (int64_t g0 = ra; g0 < rb; g0 += rg) {
-        const int n0 = (int)min<int64_t>(rg, rb - g0);  // block-uniform
-        const auto s0 = make_rsrc(src + (size_t)g0 * ld, n0 * ld * (int)sizeof(T));
-        T v0[kRepackPer];
+template <typename TS, typename TD>
+__device__ __forceinline__ void gather_rows(const TS *src, TD *dst, int64_t n, int ld, int dst_ld, int rg,
+                                            const uint32_t (&src_el)[kRepackPer],
+                                            const uint32_t (&dst_el)[kRepackPer]) {
+    constexpr int sh = sizeof(TS) == 8 ? 0 : 3;
+    for (int64_t g0 = (int64_t)blockIdx.x * rg; g0 < n; g0 += (int64_t)gridDim.x * rg) {
+        const int n0 = (int)min<int64_t>(rg, n - g0);  // block-uniform
+        const auto s0 = make_rsrc(src + (size_t)g0 * ld, n0 * ld * (int)sizeof(TS));
+        const auto d0 = make_rsrc(dst + (size_t)g0 * dst_ld, n0 * dst_ld * (int)sizeof(TD));
+        TS v0[kRepackPer];
+#if QR_DEBUG_ASSERT
+        // a slot lies inside a full group of rg rows (slots of rows j >= n0 in the last, short group
+        // fall past the buffer's range by design: their loads read 0, their stores are dropped)
+        for (int u = 0; u < kRepackPer; ++u) {
+            QR_DCHECK(src_el[u] == kRepackNone || (src_el[u] >> sh) < (uint32_t)(rg * ld * (int)sizeof(TS)), kDbgRepackSlot,
+                      src_el[u], n0);
+            QR_DCHECK(dst_el[u] == kRepackNone || (dst_el[u] >> sh) < (uint32_t)(rg * dst_ld * (int)sizeof(TD)),
+                      kDbgRepackSlot, dst_el[u], n0);
+        }
+#endif
 #pragma unroll
-        for (int u = 0; u < kRepackPer; ++u) v0[u] = rb_load(s0, src_el[u] >> (sizeof(T) == 8 ? 0 : 3), T(0));
-        loads_done_barrier();
-        const auto d0 = make_rsrc(dst + (size_t)g0 * ld, n0 * ld * (int)sizeof(T));
+        for (int u = 0; u < kRepackPer; ++u) v0[u] = rb_load(s0, src_el[u] >> sh, TS(0));
 #pragma unroll
-        for (int u = 0; u < kRepackPer; ++u) rb_store(d0, dst_el[u] >> (sizeof(T) == 8 ? 0 : 3), v0[u]);
+        for (int u = 0; u < kRepackPer; ++u) rb_store(d0, dst_el[u] >> sh, v0[u]);
     }
 }
 
-// this workgroup's contiguous share [ra, rb) of n rows
-__device__ __forceinline__ void row_share(int64_t n, int64_t &ra, int64_t &rb) {
-    ra = n * blockIdx.x / gridDim.x;
-    rb = n * (blockIdx.x + 1) / gridDim.x;
-}
-
 // The commit of a repack (by the workgroup of k_repack_rows that finishes last): frame ids, list,
-// active flags and the RangeSel.
-__device__ __forceinline__ void repack_commit(const RepackArgs &r, int cnt, int w, int w_new, bool on) {
+// active flags and the RangeSel (now in column set nb).
+__device__ __forceinline__ void repack_commit(const RepackArgs &r, int cnt, int w, int w_new, bool on, int nb) {
     const int f0 = r.f0;
     for (int p0 = 0; p0 < cnt; p0 += kRepackThreads) {
         const int p = p0 + (int)threadIdx.x;
@@ -1179,8 +1239,9 @@ __device__ __forceinline__ void repack_commit(const RepackArgs &r, int cnt, int 
         if (p < cnt) {
             const int sc = r.list[f0 + p];
             id = on ? r.fid_w[sc] : sc;  // column = frame in the caller's arrays
+            QR_DCHECK(sc >= f0 + p && sc < f0 + w && id >= 0 && id < r.ld, kDbgRepackFid, sc, id);
         }
-        loads_done_barrier();
+        loads_done_barrier();  // fid_w is compacted in place: every read of this chunk first
         if (p < cnt) {
             r.fid_w[f0 + p] = id;
             r.list[f0 + p] = f0 + p;
@@ -1196,35 +1257,42 @@ __device__ __forceinline__ void repack_commit(const RepackArgs &r, int cnt, int 
         r.sel[kSelW] = w_new;
         r.sel[kSelRepacks] += 1;
         r.sel[kSelArrive] = 0;
+        r.sel[kSelBuf] = nb;
     }
 }
 
-// The row moves of a repack: messages in place, LAPPRs / syndrome bytes from the caller's arrays
-// (first repack) or in place in the work set.  Posteriors are not moved: the range's variable sweep
-// right after rewrites every running frame's posterior in its new column; only the frames stopped
-// since the last repack hand theirs (in the work set) to the output first.  Each array's rows are
-// split into contiguous shares, one per workgroup for every chunk, so a row's chunks run in
-// ascending order.
+// The row moves of a repack.  Posteriors are not moved: the range's variable sweep right after
+// rewrites every running frame's posterior in its new column; only the frames stopped since the
+// last repack hand theirs (in the work set) to the output first.
 __global__ void __launch_bounds__(kRepackThreads) k_repack_rows(RepackArgs r) {
     int cnt, w, w_new;
-    // allocate 32 VGPRs (the code needs 22): see the register note above
+    // allocate 32 VGPRs (the code needs fewer): see the register note above
     __asm__ volatile("" ::: "v31");
     if (!repack_go(r, cnt, w, w_new)) return;  // kernel-uniform
     const bool on = sld(r.sel + kSelOn) != 0;
-    const size_t ld = r.ld;
-    const int f0 = r.f0;
-    int64_t ra, rb;
-    if (on) {  // frames stopped since the last repack hand their posteriors to the output first
-        row_share(r.V, ra, rb);
-        for (int64_t v = ra; v < rb; ++v) {
-            const double *src = r.post_w + (size_t)v * ld + f0;
-            for (int q = threadIdx.x; q < w; q += kRepackThreads) {
-                const int id = r.fid_w[f0 + q];
-                if (id >= 0 && !r.active[f0 + q]) r.out_post[(size_t)v * ld + id] = src[q];
+    const int b = on ? sld(r.sel + kSelBuf) : 0, nb = on ? 1 - b : 1;  // source / destination column set
+    const int ld = r.ld, f0 = r.f0;
+    if (on) {
+        // frames stopped since the last repack (a column < w with a frame id, no longer active)
+        // hand their posteriors to the output: slots (row j of rg, column q < w)
+        const int rg = w <= kRepackChunk / 2 ? min(16, kRepackChunk / w) : 1;
+        for (int q0 = 0; q0 < w; q0 += kRepackChunk) {
+            const int qc = min(w - q0, kRepackChunk);
+            uint32_t src_el[kRepackPer], dst_el[kRepackPer];
+#pragma unroll
+            for (int u = 0; u < kRepackPer; ++u) {
+                const int sl = u * kRepackThreads + (int)threadIdx.x;
+                const int j = sl / qc, q = q0 + sl - j * qc;
+                const int id = j < rg ? r.fid_w[f0 + q] : -1;
+                const bool go = id >= 0 && !r.active[f0 + q];
+                QR_DCHECK(id < ld, kDbgRepackFid, id, q);
+                src_el[u] = go ? (uint32_t)(j * ld + f0 + q) * 8u : kRepackNone;
+                dst_el[u] = go ? (uint32_t)(j * ld + id) * 8u : kRepackNone;
             }
+            gather_rows<double, double>(r.post_w, r.out_post, r.V, ld, ld, rg, src_el, dst_el);
         }
     }
-    // a small count moves several rows per group: rg rows x cnt columns fill the chunk's slots
+    // a small count moves several rows per group: rg rows x cnt columns fill the slots
     const int rg = cnt <= kRepackChunk / 2 ? min(16, kRepackChunk / cnt) : 1;
     for (int p0 = 0; p0 < cnt; p0 += kRepackChunk) {
         const int pc = min(cnt - p0, kRepackChunk);  // columns of this chunk (rg = 1 unless one chunk)
@@ -1234,17 +1302,17 @@ __global__ void __launch_bounds__(kRepackThreads) k_repack_rows(RepackArgs r) {
             const int sl = u * kRepackThreads + (int)threadIdx.x;
             const int j = sl / pc, q = sl - j * pc;
             const bool ok = j < rg;
-            // byte offsets in a double row group (a byte row group shifts them right by 3; an empty
-            // slot's offset stays past the group either way)
-            src_el[u] = ok ? (uint32_t)(j * (int)ld + r.list[f0 + p0 + q]) * 8u : kRepackNone;
-            dst_el[u] = ok ? (uint32_t)(j * (int)ld + f0 + p0 + q) * 8u : kRepackNone;
+            QR_DCHECK(!ok || (r.list[f0 + p0 + q] >= f0 + p0 + q && r.list[f0 + p0 + q] < f0 + w), kDbgRepackList,
+                      r.list[f0 + p0 + q], f0 + p0 + q);
+            src_el[u] = ok ? (uint32_t)(j * ld + r.list[f0 + p0 + q]) * 8u : kRepackNone;
+            dst_el[u] = ok ? (uint32_t)(j * ld + f0 + p0 + q) * 8u : kRepackNone;
         }
-        row_share(r.E, ra, rb);
-        compact_rows<double>(r.c2v, r.c2v, ra, rb, r.ld, rg, src_el, dst_el);
-        row_share(r.V, ra, rb);
-        compact_rows<double>(on ? r.lappr_w : r.lappr_in, r.lappr_w, ra, rb, r.ld, rg, src_el, dst_el);
-        row_share(r.C, ra, rb);
-        compact_rows<uint8_t>(on ? r.synd_w : r.synd_in, r.synd_w, ra, rb, r.ld, rg, src_el, dst_el);
+        // source set b, destination set nb (selects, not dynamic indices into the kernel arguments)
+        gather_rows<double, double>(b ? r.c2v[1] : r.c2v[0], nb ? r.c2v[1] : r.c2v[0], r.E, ld, ld, rg, src_el, dst_el);
+        gather_rows<double, double>(!on ? r.lappr_in : b ? r.lappr_w[1] : r.lappr_w[0], nb ? r.lappr_w[1] : r.lappr_w[0],
+                                    r.V, ld, ld, rg, src_el, dst_el);
+        gather_rows<uint8_t, uint8_t>(!on ? r.synd_in : b ? r.synd_w[1] : r.synd_w[0], nb ? r.synd_w[1] : r.synd_w[0],
+                                      r.C, ld, ld, rg, src_el, dst_el);
     }
     // the workgroup that arrives last commits: every other one has read the list, frame ids and
     // active flags it needed (its loads completed before its arrival), so the commit's rewrites of
@@ -1253,7 +1321,7 @@ __global__ void __launch_bounds__(kRepackThreads) k_repack_rows(RepackArgs r) {
     loads_done_barrier();
     if (threadIdx.x == 0) last = atomicAdd(r.sel + kSelArrive, 1) == (int)gridDim.x - 1;
     __syncthreads();
-    if (last) repack_commit(r, cnt, w, w_new, on);
+    if (last) repack_commit(r, cnt, w, w_new, on, nb);
 }
 
 
@@ -1265,6 +1333,7 @@ __global__ void k_repack_output(int64_t rows, int f0, int ld, const int32_t *sel
     if (q >= w) return;
     const int id = fid_w[f0 + q];
     if (id < 0) return;
+    QR_DCHECK(id < ld, kDbgRepackFid, id, q);
     for (int64_t v = blockIdx.y; v < rows; v += gridDim.y) out_post[(size_t)v * ld + id] = post_w[(size_t)v * ld + f0 + q];
 }
 
@@ -1280,13 +1349,16 @@ struct DecodeWs {
                      // [2] the finite flag of the input LAPPRs (first variable sweep);
                      // [4, 12) the two ranges' RangeSel (rsel)
     int32_t *rsel;
-    // the work set of the column repack (k_repack_rows, run_split2): posteriors, LAPPRs,
-    // syndrome bits and the frame id of each column of the repacked ranges (the messages are
-    // compacted in place); present when the caller's workspace has room for it (ws_bytes counts
-    // it when knob repack is on)
+    // the work set of the column repack (k_repack_rows, run_split2): posteriors and the frame id
+    // of each column of the repacked ranges, and two column sets of LAPPRs and syndrome bits (and
+    // of messages: set 0 is c2v above, set 1 c2v_alt) that consecutive repacks gather into in
+    // turn; present when the caller's workspace has room for it (ws_bytes counts it when knob
+    // repack is on)
     struct WorkSet {
-        double *post, *lappr;
-        uint8_t *synd;
+        double *post;
+        double *lappr[2];
+        uint8_t *synd[2];
+        double *c2v_alt;
         int32_t *fid;
     } rs;
     bool repack;
@@ -1307,8 +1379,8 @@ static size_t ws_base_bytes(const qr_code *code, int ld, int max_it) {
            align_up((size_t)ld * sizeof(int32_t), 256) + 256;
 }
 static size_t repack_set_bytes(const qr_code *code, int ld) {
-    return 2 * align_up((size_t)code->V * ld * sizeof(double), 256) + align_up((size_t)code->C * ld, 256) +
-           align_up((size_t)ld * sizeof(int32_t), 256);
+    return 3 * align_up((size_t)code->V * ld * sizeof(double), 256) + 2 * align_up((size_t)code->C * ld, 256) +
+           align_up((size_t)code->E * ld * sizeof(double), 256) + align_up((size_t)ld * sizeof(int32_t), 256);
 }
 static size_t ws_repack_bytes(const qr_code *code, int ld);  // after g_tune
 static size_t ws_bytes(const qr_code *code, int ld, int max_it) {
@@ -1339,14 +1411,18 @@ static DecodeWs carve(const qr_code *code, int ld, int max_it, void *base, size_
     p += 256;
     const size_t extra = ws_repack_bytes(code, ld);
     w.repack = extra > 0 && ws_size >= ws_base_bytes(code, ld, max_it) + extra;
-    w.rs = DecodeWs::WorkSet{nullptr, nullptr, nullptr, nullptr};
+    w.rs = DecodeWs::WorkSet{nullptr, {nullptr, nullptr}, {nullptr, nullptr}, nullptr, nullptr};
     if (w.repack) {
         w.rs.post = (double *)p;
         p += align_up((size_t)code->V * ld * sizeof(double), 256);
-        w.rs.lappr = (double *)p;
-        p += align_up((size_t)code->V * ld * sizeof(double), 256);
-        w.rs.synd = (uint8_t *)p;
-        p += align_up((size_t)code->C * ld, 256);
+        for (int k = 0; k < 2; ++k) {
+            w.rs.lappr[k] = (double *)p;
+            p += align_up((size_t)code->V * ld * sizeof(double), 256);
+            w.rs.synd[k] = (uint8_t *)p;
+            p += align_up((size_t)code->C * ld, 256);
+        }
+        w.rs.c2v_alt = (double *)p;
+        p += align_up((size_t)code->E * ld * sizeof(double), 256);
         w.rs.fid = (int32_t *)p;
     }
     return w;
@@ -1357,7 +1433,7 @@ struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3},
         lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024}, var_pace{28},
         check_tail{4}, fused_iter{1}, iter_streams{2}, var_boost{4}, resident{1}, repack{1},
-        repack_pct{50};
+        repack_pct{50}, repack_grid{512};
 };
 static Tuning g_tune;
 
@@ -1439,7 +1515,9 @@ struct Plan {
         a.per_t = a.g.per;
         a.sel = sel_of(f0);
         a.post_w = w.rs.post;
-        a.synd_w = w.rs.synd;
+        a.synd_w[0] = w.rs.synd[0];
+        a.synd_w[1] = w.rs.synd[1];
+        a.c2v_alt = w.rs.c2v_alt;
         return a;
     }
     VarArgs var_args(int f0, int f1) const {
@@ -1464,8 +1542,10 @@ struct Plan {
         a.fin_bound = 0.0;
         a.fin_B = 0;
         a.sel = sel_of(f0);
-        a.lappr_w = w.rs.lappr;
+        a.lappr_w[0] = w.rs.lappr[0];
+        a.lappr_w[1] = w.rs.lappr[1];
         a.post_w = w.rs.post;
+        a.c2v_alt = w.rs.c2v_alt;
         return a;
     }
 };
@@ -1736,19 +1816,21 @@ static int launch_repack(const Plan &P, int f0, int h) {
     r.sel = P.w.rsel + (f0 == 0 ? 0 : kSelInts);
     r.list = P.w.alist;
     r.active = P.w.active;
-    r.c2v = P.w.c2v;
+    r.c2v[0] = P.w.c2v;
+    r.c2v[1] = P.w.rs.c2v_alt;
     r.out_post = P.post;
     r.lappr_in = P.lappr;
     r.synd_in = P.synd;
     r.post_w = P.w.rs.post;
-    r.lappr_w = P.w.rs.lappr;
-    r.synd_w = P.w.rs.synd;
+    for (int k = 0; k < 2; ++k) {
+        r.lappr_w[k] = P.w.rs.lappr[k];
+        r.synd_w[k] = P.w.rs.synd[k];
+    }
     r.fid_w = P.w.rs.fid;
-    const int64_t rows = code->E + 2 * code->V + code->C;
     ProfScope ps("repack", P.s);
-    // kRepackGrid workgroups walk the rows; when the device decides not to repack they all leave
-    // at once (a few microseconds on the variable stream)
-    k_repack_rows<<<(unsigned)std::min<int64_t>(rows, kRepackGrid), kRepackThreads, 0, P.s>>>(r);
+    // repack_grid workgroups walk the row groups; when the device decides not to repack they all
+    // leave at once (a few microseconds on the variable stream)
+    k_repack_rows<<<(unsigned)std::clamp(g_tune.repack_grid.load(), 1, 4096), kRepackThreads, 0, P.s>>>(r);
     QR_LAUNCH_CHECK();
     return QR_OK;
 }
@@ -1858,7 +1940,7 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
         const int f0 = k * h;
         if ((rc = launch_checks<kParityOnly>(F, P.post, unsat_last, f0, f0 + h))) return rc;
         if ((rc = launch_status(F, f0, f0 + h, max_it, 1, max_it, unsat_last))) return rc;
-        ProfScope ps("repack", P.s);
+        ProfScope ps("repack_out", P.s);
         k_repack_output<<<dim3((unsigned)(h + 255) / 256, (unsigned)std::min<int64_t>(code->V, 2048)), 256, 0, P.s>>>(
             code->V, f0, ld, F.sel_of(f0), P.w.rs.fid, P.w.rs.post, P.post);
         QR_LAUNCH_CHECK();
@@ -1953,8 +2035,11 @@ static bool resident_code(const qr_code *code) {
 }
 
 static int run_resident(const qr_code *code, int B, int ld, const double *lappr, const uint8_t *synd, int max_it,
-                        double *final_post, uint8_t *success, int32_t *iters, hipStream_t s) {
+                        double *final_post, uint8_t *success, int32_t *iters, int32_t *rsel, hipStream_t s) {
     ResArgs a;
+    a.rsel = rsel;
+    a.w0 = ld / 2;
+    a.w1 = ld - ld / 2;
     a.C = (int)code->C;
     a.V = (int)code->V;
     a.B = B;
@@ -2002,7 +2087,8 @@ int decode_batch_device(const qr_code *code, int B, int ld, const double *lappr,
                          ws_base_bytes(code, ld, max_it));
     DeviceGuard dg(code->device);
     if (max_it > 0 && max_it <= kResMaxIter && resident_code(code))
-        return run_resident(code, B, ld, lappr, synd, max_it, final_post, success, iters, s);
+        return run_resident(code, B, ld, lappr, synd, max_it, final_post, success, iters,
+                            carve(code, ld, max_it, ws_ptr, ws_size).rsel, s);
     Plan P{code, B, ld, lappr, synd, final_post, success, iters, carve(code, ld, max_it, ws_ptr, ws_size), g_tune.nt.load() != 0, s};
     const int64_t rows = (int64_t)(max_it > 0 ? max_it : 0) + 2;  // no int overflow at INT_MAX
     int rc;
@@ -2241,6 +2327,20 @@ int qr_code_create(const int64_t *e_to_v, const int64_t *e_to_c, int64_t nv, int
 
 int qr_code_destroy(qr_code *code) { return free_code(code); }
 
+#if QR_DEBUG_ASSERT
+// Debug build only (libqamr_debug.so; not in include/qamr.h): out = {failed device checks, first
+// failing site (DebugSite), its two values}; reads and clears them.
+QR_API int qr_debug_asserts(int64_t *out) {
+    unsigned long long h[4] = {0, 0, 0, 0};
+    if (hipDeviceSynchronize() != hipSuccess) return QR_EDEVICE;
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(qr::g_dbg), sizeof(h)) != hipSuccess) return QR_EDEVICE;
+    const unsigned long long z[4] = {0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(qr::g_dbg), z, sizeof(z)) != hipSuccess) return QR_EDEVICE;
+    for (int i = 0; i < 4; ++i) out[i] = (int64_t)h[i];
+    return QR_OK;
+}
+#endif
+
 #if QR_EXPERIMENT_CLOCK
 // Diagnostic builds only (not in include/qamr.h): out = {sum cycles, sum ticks, workgroups}.
 QR_API int qr_debug_clock(int64_t *out) {
@@ -2272,7 +2372,7 @@ static std::atomic<int> *tune_knob(const char *name) {
         {"var_pace", &g_tune.var_pace},     {"check_tail", &g_tune.check_tail}, {"var_boost", &g_tune.var_boost},
         {"fused_iter", &g_tune.fused_iter}, {"iter_streams", &g_tune.iter_streams},
         {"resident", &g_tune.resident},   {"repack", &g_tune.repack},
-        {"repack_pct", &g_tune.repack_pct},
+        {"repack_pct", &g_tune.repack_pct}, {"repack_grid", &g_tune.repack_grid},
     };
     const std::string n = name ? name : "";
     for (const auto &k : knobs)

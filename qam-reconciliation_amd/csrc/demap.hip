@@ -67,6 +67,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kDemap
 // owner sums its M terms in m order (noisemapper.pyx:278-286: the same products, the same
 // sequence of additions).
 constexpr int kDemapWaveMaxBps = 6;
+#if QR_EXPERIMENT_CLOCK
+// the in-kernel clock of the wave-private demapper's launches (diagnostic twin only): {cycles,
+// ticks, workgroups}, read and cleared by qr_debug_clock_demap
+__device__ unsigned long long g_clk_demap[3];
+#endif
 // LLR-sum loop unroll of k_demap_wave (1 / 16: 50.3 / 57.0 ms vs 46.8 at 4, 16-PAM, round 3)
 constexpr int kDemapUnroll = 4;
 
@@ -129,11 +134,14 @@ __device__ __forceinline__ double g_inv_search_wave(const DemapTables &t, const 
 // 127 VGPRs, 4 waves/SIMD.  Forced to 5 / 6 waves (96 / 80 VGPRs, 108 / 160 B spilled per lane):
 // 16-PAM 44.2-44.3 / 44.6-44.7 ms vs 44.0-44.1, 4-PAM 16.9 / 19.1 ms vs 13.7 (MI355X, B = 4096).
 template <int BPS>
-__global__ void __launch_bounds__(256) k_demap_wave(const DemapTables *__restrict__ tab,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_demap_wave(const DemapTables *__restrict__ tab,
                                                     const MathTables *__restrict__ gmt, int B, int ld, int64_t S,
                                                     const double *__restrict__ n, const int64_t *__restrict__ j,
                                                     double alpha, double *__restrict__ lappr) {
     constexpr int M = 1 << BPS;
+#if QR_EXPERIMENT_CLOCK
+    ClkScope clk(true, g_clk_demap, nullptr);  // (diagnostic twin only)
+#endif
     __shared__ GlibcExpLog gt;
     __shared__ double ey[4][64], et[4][64];
     __shared__ double acc[4][2 * BPS][64];   // per wave: N[k] rows then D[k] rows, lane = frame
@@ -151,20 +159,27 @@ __global__ void __launch_bounds__(256) k_demap_wave(const DemapTables *__restric
         const int64_t jv = valid ? j[s * ld + f] : 0;
         const bool jok = jv >= 0 && jv < M;
         const int jj = jok ? (int)jv : 0;
-        const double aj = t.a[jj];
+        const double aj = t.a[jj], pj = t.p[jj];
 #pragma unroll
         for (int k = 0; k < 2 * BPS; ++k) accw[k * 64 + lane] = 0.0;
 #pragma unroll 1
         for (int i = 0; i < M; ++i) {
             const double y = g_inv_search_wave<M>(t, *gmt, nv, i, ey[w], et[w], lane);
-            // noisemapper.pyx:503-515 in the reference's summation order (k < j, p[j], k > j)
+            // noisemapper.pyx:503-515 in the reference's summation order (k < j, p[j], k > j).
+            // Straight-line: every lane computes both exponents (e, and e / 2 sigma^2 for k > j)
+            // and selects -- the lanes of a wave hold different j, so a branch around the
+            // division ran for nearly every k anyway, plus its exec-mask bookkeeping -- and
+            // p[j] is the lane's own, loaded once per tile.
             double sum = 0;
 #pragma unroll kDemapUnroll
             for (int k = 0; k < M; ++k) {
-                const double e = (2 * y - t.a[k] - aj) * (t.a[k] - aj);
-                const double arg = k < jj ? e : k == jj ? 1.0 : div_two_s2(t, e);
+                const double ak = t.a[k];
+                const double e = (2 * y - ak - aj) * (ak - aj);
+                const double ed = div_two_s2(t, e);
+                const double arg = k < jj ? e : k == jj ? 1.0 : ed;
                 const double ex = g_exp_wave(arg, gt);
-                sum += k == jj ? t.p[jj] : ex * t.p[k];
+                const double tk = ex * t.p[k];
+                sum += k == jj ? pj : tk;
             }
             const double q = t.dF[i] / sum;
             int mi = i;
@@ -445,6 +460,19 @@ int demap_batch_device(const qr_demap *dm, int B, int ld, int64_t S, const doubl
 using namespace qr;
 
 extern "C" {
+
+#if QR_EXPERIMENT_CLOCK
+// Diagnostic builds only (not in include/qamr.h): out = {sum cycles, sum ticks, workgroups} of the
+// wave-private demapper's stamped launches since the last call.
+QR_API int qr_debug_clock_demap(int64_t *out) {
+    unsigned long long h[3] = {0, 0, 0};
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(qr::g_clk_demap), sizeof(h)) != hipSuccess) return QR_EDEVICE;
+    const unsigned long long z[3] = {0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(qr::g_clk_demap), z, sizeof(z)) != hipSuccess) return QR_EDEVICE;
+    for (int i = 0; i < 3; ++i) out[i] = (int64_t)h[i];
+    return QR_OK;
+}
+#endif
 
 int qr_demap_create(int32_t bps, const double *constellation, const double *probabilities, const double *thresholds,
                     double noise_var, const uint8_t *sign_config, int32_t device, qr_demap **out) {

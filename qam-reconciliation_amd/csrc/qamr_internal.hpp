@@ -76,6 +76,41 @@ struct DeviceGuard {
     int prev_ = 0, dev_ = 0;
 };
 
+// Diagnostic twin only (libqamr_clock.so, QR_EXPERIMENT_CLOCK=1; the product library carries no
+// stamp): a workgroup's shader-clock (s_memtime) and 100 MHz realtime (s_memrealtime) spans added
+// to acc[0..2] = {cycles, ticks, workgroups} by thread 0 (vector atomics) when the scope ends, and
+// its realtime start / end stored in wgt (first kWgTimes workgroups) if given.  Every thread of
+// the workgroup must reach the end of the scope (it ends with a barrier).
+#ifndef QR_EXPERIMENT_CLOCK
+#define QR_EXPERIMENT_CLOCK 0
+#endif
+constexpr int kWgTimes = 1 << 16;
+#if QR_EXPERIMENT_CLOCK
+struct ClkScope {
+    bool on;
+    unsigned long long *acc, *wgt;
+    uint64_t c0, r0;
+    __device__ ClkScope(bool on_, unsigned long long *acc_, unsigned long long *wgt_) : on(on_), acc(acc_), wgt(wgt_) {
+        c0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    __device__ ~ClkScope() {
+        __syncthreads();
+        if (on && threadIdx.x == 0) {
+            const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+            atomicAdd(&acc[0], (unsigned long long)(c1 - c0));
+            atomicAdd(&acc[1], (unsigned long long)(r1 - r0));
+            atomicAdd(&acc[2], 1ull);
+            const unsigned b = blockIdx.y * gridDim.x + blockIdx.x;
+            if (wgt && b < (unsigned)kWgTimes) {
+                wgt[2 * b] = r0;
+                wgt[2 * b + 1] = r1;
+            }
+        }
+    }
+};
+#endif
+
 }  // namespace qr
 
 // --------------------------------------------------------------- handles

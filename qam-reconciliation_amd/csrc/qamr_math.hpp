@@ -370,6 +370,9 @@ QR_HD void F_and_density(const DemapTables &t, const MathTables &mt, double y, d
 // F_Y and f_Y from the Taylor table (Newton only): ~30 FMA instead of M erf.  Returns
 // false outside the table.
 constexpr int kFtabDeg = 12;
+#ifndef QR_FTAB_HOLD
+#define QR_FTAB_HOLD(x) __asm__ volatile("" : "+v"(x))
+#endif
 constexpr int kFtabStride = 16;   // doubles per interval (128 B)
 QR_HD bool F_and_density_tab(const DemapTables &t, double y, double &F, double &f) {
     const double x = (y - t.ftab_lo) * t.ftab_inv_w;
@@ -378,7 +381,25 @@ QR_HD bool F_and_density_tab(const DemapTables &t, double y, double &F, double &
     // exact: h is a power of two and lo a multiple of 2h, so the centre and y - centre
     // are exact doubles (u may leave [-1, 1] by an ulp at the interval ends)
     const double u = (y - (t.ftab_lo + (2 * j + 1) * t.ftab_h)) * t.ftab_inv_h;
+#ifdef __HIP_DEVICE_COMPILE__
+    // all kFtabDeg + 1 coefficients (one 128-B row) requested at once, as global (not flat) loads,
+    // and held until the last has arrived: one memory round trip per evaluation instead of the
+    // compiler's seven (it issued each 16-B piece right before its Horner step, each behind a
+    // vmcnt(0) lgkmcnt(0) wait)
+    typedef __attribute__((address_space(1))) const double2 gdouble2;
+    gdouble2 *C2 = (gdouble2 *)(t.ftab + (size_t)j * kFtabStride);
+    double C[kFtabStride];
+#pragma unroll
+    for (int q = 0; q < (kFtabDeg + 2) / 2; ++q) {
+        const double2 v = C2[q];
+        C[2 * q] = v.x;
+        C[2 * q + 1] = v.y;
+    }
+#pragma unroll
+    for (int q = 0; q <= kFtabDeg; ++q) QR_FTAB_HOLD(C[q]);
+#else
     const double *C = t.ftab + (size_t)j * kFtabStride;
+#endif
     double F_ = C[kFtabDeg], d = kFtabDeg * C[kFtabDeg];
     for (int k = kFtabDeg - 1; k >= 1; --k) {
         F_ = __builtin_fma(F_, u, C[k]);

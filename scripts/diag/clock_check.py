@@ -9,8 +9,9 @@ hipEvents, for the default two-stream schedule and any QAMR_TUNE-style variants.
 Per variant: step ms, check_d7 launch us (events), effective clock GHz, and the VALU issue
 fraction at that clock (1.585e9 wave-instructions x 4 cycles / 1024 SIMDs per 2048-frame
 launch, scaled by the launch's frames).
-  --json [--workload W --batch B]: one JSON line {"clock_ghz", "launch_us", "workgroups"} for
-the default tuning (QAMR_TUNE applies), read by bench.py's roofline."""
+  --json [--workload W --batch B --snr S --key K]: one JSON line {"clock_ghz", "launch_us",
+"workgroups"} of the launches of profile key K (check_d7, resident_d6 or demap) for the default
+tuning (QAMR_TUNE applies), read by bench.py's rooflines."""
 import ctypes as C
 import os
 import sys
@@ -28,24 +29,27 @@ from qamr import _lib  # noqa: E402
 VALU_PER_FRAME = 1.585e9 / 2048  # wave-instructions of one check_d7 launch per frame (PMC, r03)
 
 
-def run(variant, w, L, steps=4, quiet=False):
+def run(variant, w, L, steps=4, quiet=False, key="check_d7"):
     for item in filter(None, variant.split(",")):
         k, v = item.split("=")
         _lib.tune_set(k.strip(), int(v))
+    # the stamped kernels: degree-7 check sweep and frame-resident decode (qr_debug_clock), the
+    # wave-private demapper (qr_debug_clock_demap)
+    read = L.qr_debug_clock_demap if key == "demap" else L.qr_debug_clock
     w.step_eager()
     w.sync()
     out = (C.c_int64 * 3)()
-    L.qr_debug_clock(out)  # clear
+    read(out)  # clear
     _lib.profile_enable(True)
-    _lib.profile_select("check_d7")
+    _lib.profile_select(key)
     _lib.profile_reset()
     t0 = time.perf_counter()
     for _ in range(steps):
         w.step_eager()
     w.sync()
     dt = (time.perf_counter() - t0) / steps
-    ms, n = _lib.profile_query("check_d7")
-    L.qr_debug_clock(out)
+    ms, n = _lib.profile_query(key)
+    read(out)
     _lib.profile_enable(False)
     cyc, ticks, blocks = out[0], out[1], out[2]
     ghz = cyc / ticks * 0.1 if ticks else float("nan")
@@ -53,7 +57,8 @@ def run(variant, w, L, steps=4, quiet=False):
     frames = w.B if _lib.tune_get("split") < 2 else w.B // 2
     issue_us = VALU_PER_FRAME * frames * 4 / 1024 / (ghz * 1e3)
     if quiet:
-        return {"clock_ghz": round(ghz, 4), "launch_us": round(launch_us, 1), "workgroups": blocks, "steps": steps}
+        return {"clock_ghz": round(ghz, 4), "launch_us": round(launch_us, 1), "workgroups": blocks, "steps": steps,
+                "kernel_key": key}
     print(f"variant '{variant or 'default'}': step {dt * 1e3:.1f} ms, {w.B / dt:.0f} frames/s, check_d7 "
           f"{launch_us:.0f} us x {n}, clock {ghz:.3f} GHz ({blocks} workgroups), VALU issue {issue_us:.0f} us "
           f"= {issue_us / launch_us:.3f} of the launch", flush=True)
@@ -94,9 +99,10 @@ def wg_times(w, L, steps=2):
 def main():
     L = _lib.load()
     L.qr_debug_clock.argtypes = [C.c_void_p]
+    L.qr_debug_clock_demap.argtypes = [C.c_void_p]
     argv = sys.argv[1:]
     as_json = "--json" in argv
-    opts = {"--workload": "dvbs2_4pam", "--batch": "4096"}
+    opts = {"--workload": "dvbs2_4pam", "--batch": "4096", "--key": "check_d7", "--snr": ""}
     for k in opts:
         if k in argv:
             i = argv.index(k)
@@ -105,12 +111,13 @@ def main():
     argv = [a for a in argv if a not in ("--json",)]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    w = bench.Work(opts["--workload"], None, int(opts["--batch"]), 50, 1.0, 0, 0, 0)
+    w = bench.Work(opts["--workload"], float(opts["--snr"]) if opts["--snr"] else None, int(opts["--batch"]), 50, 1.0,
+                   0, 0, 0)
     w.step_eager()
     w.sync()
     if as_json:
         import json
-        print(json.dumps(run("", w, L, quiet=True)), flush=True)
+        print(json.dumps(run("", w, L, quiet=True, key=opts["--key"])), flush=True)
         return
     if "--wgtimes" in argv:
         wg_times(w, L)

@@ -1,14 +1,16 @@
 #!/usr/bin/env python3
 """Summarise a scripts/profile_session.sh output directory.
 
-    python scripts/summarize_profile.py gpurun_out/prof_r1 [--kernel 'k_fused<7, 1, true, 0>'] [--math 0]
+    python scripts/summarize_profile.py gpurun_out/prof_r1 [--kernel 'k_check<7, 1, true>'] [--kernel-key check_d7]
+        [--workload dvbs2_4pam --batch 4096] [--source TEXT] [--into profiles/pmc_secondary.json]
 
 Writes <dir>/summary.md (per-kernel time from --kernel-trace --stats, PMC counters
 per launch) and <dir>/pmc_traffic.json: HBM bytes per launch of the dominant
 kernel = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 -- the gfx950 corrections of
 MI355X_MICROARCH.md 'HBM': FETCH_SIZE (KiB) counts half the bytes of wide
 coalesced reads (calibrated here on the variable sweep, whose read bytes are
-known exactly), WRITE_SIZE (KiB) is exact.
+known exactly), WRITE_SIZE (KiB) is exact.  --into merges the record into a JSON list of such
+records (one per workload, batch and kernel key: bench.py's pmc_entry reads them).
 """
 import argparse
 import collections
@@ -25,9 +27,10 @@ def short(name):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--kernel", default="k_fused<7, 1, true, 0>")
-    ap.add_argument("--math", type=int, default=0, help="decoder arithmetic (knob math) of the profiled run")
-    ap.add_argument("--kernel-key", default="fused_d7")
+    ap.add_argument("--kernel", default="k_check<7, 1, true>")
+    ap.add_argument("--kernel-key", default="check_d7")
+    ap.add_argument("--source", default=None, help="provenance text stored in the record")
+    ap.add_argument("--into", default=None, help="JSON list of records to merge this one into")
     ap.add_argument("--workload", default="dvbs2_4pam")
     ap.add_argument("--batch", type=int, default=4096)
     args = ap.parse_args()
@@ -60,7 +63,6 @@ def main():
         fetch = sum(kc["FETCH_SIZE"]) / len(kc["FETCH_SIZE"])
         write = sum(kc["WRITE_SIZE"]) / len(kc["WRITE_SIZE"])
         out = {"workload": args.workload, "batch": args.batch, "kernel": args.kernel, "kernel_key": args.kernel_key,
-               "math": args.math,
                "fetch_size_kib": fetch, "write_size_kib": write,
                "hbm_bytes_per_launch": int((2 * fetch + write) * 1024),
                "correction": "2*FETCH_SIZE + WRITE_SIZE, KiB -> bytes (MI355X_MICROARCH.md HBM section)",
@@ -82,7 +84,17 @@ def main():
             out["valu_busy_pmc"] = avg("SQ_ACTIVE_INST_VALU") / cus / grbm_xcd
             if avg_ns.get(args.kernel):
                 out["clock_ghz_pmc"] = grbm_xcd / avg_ns[args.kernel]
+        if args.source:
+            out["source"] = args.source
         json.dump(out, open(os.path.join(d, "pmc_traffic.json"), "w"), indent=1)
+        if args.into:
+            try:
+                recs = json.load(open(args.into))
+            except Exception:
+                recs = []
+            recs = [r for r in recs if (r.get("workload"), r.get("batch"), r.get("kernel_key"))
+                    != (out["workload"], out["batch"], out["kernel_key"])] + [out]
+            json.dump(recs, open(args.into, "w"), indent=1)
         lines.append(f"\nDominant kernel `{args.kernel}`: HBM traffic per launch "
                      f"{out['hbm_bytes_per_launch'] / 1e9:.2f} GB (2*FETCH + WRITE)")
     open(os.path.join(d, "summary.md"), "w").write("\n".join(lines) + "\n")

@@ -71,3 +71,25 @@ def assert_bit_exact(got, ref):
         k = np.flatnonzero(diff)[0]
         raise AssertionError(f"{diff.sum()} of {m.sum()} values differ; first: got {got[m][k]!r} ref {ref[m][k]!r} "
                              f"(|d| = {abs(got[m][k] - ref[m][k]):.3e})")
+
+
+# Debug-build runs (tests/test_gpu_debug_build.py): with QAMR_DEBUG_ASSERTS=1 the process has
+# loaded libqamr_debug.so (QAMR_LIB) and every test must leave its device index checks unfailed.
+@pytest.fixture(autouse=True)
+def _device_checks(request):
+    if os.environ.get("QAMR_DEBUG_ASSERTS") != "1" or request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    import ctypes
+
+    from qamr import _lib
+
+    L = _lib.load()
+    assert hasattr(L, "qr_debug_asserts"), "QAMR_DEBUG_ASSERTS=1 but the debug library is not loaded"
+    fn = L.qr_debug_asserts
+    fn.argtypes = [ctypes.c_void_p]
+    out = (ctypes.c_int64 * 4)()
+    assert fn(out) == 0
+    yield
+    assert fn(out) == 0
+    assert out[0] == 0, f"{out[0]} device index checks failed; first: site {out[1]} values {out[2]}, {out[3]}"

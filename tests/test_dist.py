@@ -108,6 +108,7 @@ def _check_world2(out):
     B = out["config"]["batch_per_gpu"]
     # StubWork rank r contributes [10(r+1), r+1, B-r-1, 7(B-r-1), B]: the line carries the sums
     assert out["counters"] == [10 + 20, 1 + 2, (B - 1) + (B - 2), 7 * ((B - 1) + (B - 2)), 2 * B]
+    assert len(out["per_rank"]["ms_per_step"]) == 2
     # value = frames of all ranks / max-over-ranks timed region
     assert abs(out["value"] - 2 * B * out["steps"] / (out["ms_per_step"] * out["steps"] / 1e3)) / out["value"] < 1e-2
 
@@ -219,6 +220,12 @@ def _check_world8(out):
     # StubWork rank r contributes [10(r+1), r+1, B-r-1, 7(B-r-1), B]
     assert out["counters"] == [10 * 36, 36, 8 * B - 36, 7 * (8 * B - 36), 8 * B]
     assert out["config"]["rank_devices"] == list(range(8))     # rank r bound LOCAL_RANK r
+    # the per-rank record of the first scaling run: every rank's own timed region, the line's
+    # ms_per_step their max (the stub has no priced kernel: no event averages)
+    pr = out["per_rank"]
+    assert len(pr["ms_per_step"]) == 8 and all(v > 0 for v in pr["ms_per_step"])
+    assert abs(max(pr["ms_per_step"]) - out["ms_per_step"]) <= 1e-3 * out["ms_per_step"] + 1e-3
+    assert pr["avg_launch_us"] == [None] * 8 and pr["priced_kernel"] is None
 
 
 def test_bench_gpus8_self_launch():

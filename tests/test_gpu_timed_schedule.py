@@ -126,12 +126,15 @@ def test_reference_frames_in_timed_batch(gpu, fname, key, bps, snr, B):
                                           (2, 4.0, 1024, 22)])
 def test_column_repack_vs_oracle(gpu, bps, snr, B, mi):
     """Converging batches under the column repack (knob repack, default on: when a range's
-    running frames fill at most repack_pct = 75 % of its columns, the device moves them to the
-    front of the range), incl. the bench's own B = 4096 batches of its converging operating
-    points (BENCH op_dvbs2_4pam_4.0dB / op_dvbs2_16pam_14.5dB): every frame identical to the
-    run with no repack at all, the frames that ran longest --
-    the ones that went through the repacks -- and frames spread over both ranges bit-exact
-    against the oracle, and the device did repack (reference: decoder.pyx:424-436)."""
+    running frames fill at most knob repack_pct percent of its columns, the device gathers them
+    into the front columns of the work set's other column set), incl. the bench's own B = 4096
+    batches of its converging operating points (BENCH op_dvbs2_4pam_4.0dB /
+    op_dvbs2_16pam_14.5dB): every frame identical to the run with no repack at all, the frames
+    that ran longest -- the ones that went through the repacks -- and frames spread over both
+    ranges bit-exact against the oracle, and the device did repack.  On the bench's 4-PAM
+    4.0 dB batch a range repacks more than once (column set 1 -> 0 as well as 0 -> 1) and ends
+    at most 64 columns wide, so its last iterations ran the narrow sweeps (lanes = node x
+    frame, check_narrow / var_narrow_sweep) (reference: decoder.pyx:424-436)."""
     import torch
     from qamr import _lib
 
@@ -152,6 +155,9 @@ def test_column_repack_vs_oracle(gpu, bps, snr, B, mi):
     assert rep0 + rep1 > 0, stats[0]                  # the device repacked
     assert min(w0, w1) < pipe.ld // 2, stats[0]
     assert stats[1] == ((0, 0), (pipe.ld // 2, pipe.ld // 2))  # repack off: never
+    if (bps, snr, B) == (2, 4.0, 4096):
+        assert max(rep0, rep1) >= 2, stats[0]  # both directions between the column sets
+        assert min(w0, w1) <= 64, stats[0]     # the narrow sweeps ran
     f1, s1, i1 = outs[0]
     for f0, s0, i0 in outs[1:]:
         assert torch.equal(s1, s0) and torch.equal(i1, i0)
@@ -209,3 +215,25 @@ def test_repack_decode_is_asynchronous_and_capturable(gpu):
     assert sum(graph_stats[0]) > 0, graph_stats
     assert torch.equal(succ, ref[1]) and torch.equal(its, ref[2])
     assert torch.equal(fin[:, :B].view(torch.int64), ref[0][:, :B].view(torch.int64))
+
+
+def test_repack_stats_after_resident_decode(gpu):
+    """qr_decode_repack_stats reports "never repacked" (0 repacks, widths ld / 2) for a decode
+    that took the frame-resident schedule (configs[1]'s reg-(3,6) N=1008), even on a workspace
+    whose last two-stream decode did repack."""
+    import torch
+    import qamr
+    from qamr import codes
+    from qamr.pipeline import SofteningPipeline
+
+    vid, cid = codes.regular_code(1008)
+    dec = qamr.Decoder(vid, cid)
+    pipe = SofteningPipeline(dec, bps=2, snr_db=3.0, batch=1024, max_iterations=20)
+    b = pipe.generate(torch.Generator(device="cuda").manual_seed(5))
+    lappr = pipe.demap(b)
+    st = torch.cuda.current_stream()
+    ws = dec._workspace(st, dec.workspace_bytes(pipe.ld, 20))
+    ws.fill_(0x5A)  # garbage where the RangeSel block lives
+    pipe.decode(lappr, b)
+    torch.cuda.synchronize()
+    assert dec.repack_stats(pipe.ld, 20) == ((0, 0), (pipe.ld // 2, pipe.ld // 2))
