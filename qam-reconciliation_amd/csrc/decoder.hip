@@ -205,6 +205,10 @@ struct VarArgs {
     const double *lappr_w[2];
     double *post_w;
     const double *c2v_alt;
+    // knob var_list_pct: the sweep follows the active-frame list only when the running frames fill
+    // at most this percentage of the range's columns (else lane = column, stopped frames skipped
+    // by their flag); 100 = always
+    int list_pct;
 };
 
 // The state of one frame range of the two-stream schedule, in device memory (the workspace's
@@ -574,6 +578,21 @@ __global__ void __launch_bounds__(256) k_var(VarArgs a) {
     if (!INIT && range_narrow(a.sel, a.acount)) {  // kernel-uniform
         var_narrow_sweep(a);
         return;
+    }
+    // A partly stopped range: the list maps the lanes of a wave to scattered columns, so each wave
+    // reads ~1.5x the cache lines of a dense wave for the same bytes, and this sweep is bound by
+    // those lines (MI355X, 4-PAM 4.0 dB: 4.4-4.8 ms per sweep of a range with ~70 % of its frames
+    // running, against 3.5 ms dense; the check sweep beside it, VALU-bound, gains from the list).
+    // While most columns still run, sweep the columns themselves (kernel-uniform): the stopped
+    // frames' lanes load and skip their store (their flag), every wave reads 64 consecutive columns.
+    if (!INIT && a.alist && a.list_pct < 100) {
+        const int cnt = sld(a.acount);
+        const int w = (a.sel && sld(a.sel + kSelOn)) ? sld(a.sel + kSelW) : (int)(a.nby << a.g.lft);
+        if ((int64_t)cnt * 100 > (int64_t)w * a.list_pct) {
+            a.alist = nullptr;
+            a.acount = nullptr;
+            a.nby = min(a.nby, (unsigned)((w + (1 << a.g.lft) - 1) >> a.g.lft));
+        }
     }
     if (a.gs) {  // capped grid: tile t = (bx fastest, by), the grid's blocks sweep a moving window
         unsigned ny = a.nby, stride = gridDim.x;
@@ -1207,11 +1226,18 @@ __device__ __forceinline__ void gather_rows(const TS *src, TD *dst, int64_t n, i
                                             const uint32_t (&src_el)[kRepackPer],
                                             const uint32_t (&dst_el)[kRepackPer]) {
     constexpr int sh = sizeof(TS) == 8 ? 0 : 3;
-    for (int64_t g0 = (int64_t)blockIdx.x * rg; g0 < n; g0 += (int64_t)gridDim.x * rg) {
-        const int n0 = (int)min<int64_t>(rg, n - g0);  // block-uniform
+    // two row groups per step: the loads of both are in flight together (the moves are bound by
+    // the memory round trip of each step, not by bandwidth)
+    const int64_t stride = (int64_t)gridDim.x * rg;
+    for (int64_t g0 = (int64_t)blockIdx.x * rg; g0 < n; g0 += 2 * stride) {
+        const int64_t g1 = g0 + stride;
+        const int n0 = (int)min<int64_t>(rg, n - g0);                       // block-uniform
+        const int n1 = g1 < n ? (int)min<int64_t>(rg, n - g1) : 0;          // (0: no second group)
         const auto s0 = make_rsrc(src + (size_t)g0 * ld, n0 * ld * (int)sizeof(TS));
         const auto d0 = make_rsrc(dst + (size_t)g0 * dst_ld, n0 * dst_ld * (int)sizeof(TD));
-        TS v0[kRepackPer];
+        const auto s1 = make_rsrc(src + (size_t)(n1 ? g1 : g0) * ld, n1 * ld * (int)sizeof(TS));
+        const auto d1 = make_rsrc(dst + (size_t)(n1 ? g1 : g0) * dst_ld, n1 * dst_ld * (int)sizeof(TD));
+        TS v0[kRepackPer], v1[kRepackPer];
 #if QR_DEBUG_ASSERT
         // a slot lies inside a full group of rg rows (slots of rows j >= n0 in the last, short group
         // fall past the buffer's range by design: their loads read 0, their stores are dropped)
@@ -1225,7 +1251,11 @@ __device__ __forceinline__ void gather_rows(const TS *src, TD *dst, int64_t n, i
 #pragma unroll
         for (int u = 0; u < kRepackPer; ++u) v0[u] = rb_load(s0, src_el[u] >> sh, TS(0));
 #pragma unroll
+        for (int u = 0; u < kRepackPer; ++u) v1[u] = rb_load(s1, src_el[u] >> sh, TS(0));
+#pragma unroll
         for (int u = 0; u < kRepackPer; ++u) rb_store(d0, dst_el[u] >> sh, v0[u]);
+#pragma unroll
+        for (int u = 0; u < kRepackPer; ++u) rb_store(d1, dst_el[u] >> sh, v1[u]);
     }
 }
 
@@ -1433,7 +1463,7 @@ struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3},
         lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024}, var_pace{28},
         check_tail{4}, fused_iter{1}, iter_streams{2}, var_boost{4}, resident{1}, repack{1},
-        repack_pct{50}, repack_grid{512};
+        repack_pct{50}, repack_grid{512}, var_list_pct{100};
 };
 static Tuning g_tune;
 
@@ -1546,6 +1576,7 @@ struct Plan {
         a.lappr_w[1] = w.rs.lappr[1];
         a.post_w = w.rs.post;
         a.c2v_alt = w.rs.c2v_alt;
+        a.list_pct = std::clamp(g_tune.var_list_pct.load(), 0, 100);
         return a;
     }
 };
@@ -2373,6 +2404,7 @@ static std::atomic<int> *tune_knob(const char *name) {
         {"fused_iter", &g_tune.fused_iter}, {"iter_streams", &g_tune.iter_streams},
         {"resident", &g_tune.resident},   {"repack", &g_tune.repack},
         {"repack_pct", &g_tune.repack_pct}, {"repack_grid", &g_tune.repack_grid},
+        {"var_list_pct", &g_tune.var_list_pct},
     };
     const std::string n = name ? name : "";
     for (const auto &k : knobs)

@@ -164,23 +164,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         for (int k = 0; k < 2 * BPS; ++k) accw[k * 64 + lane] = 0.0;
 #pragma unroll 1
         for (int i = 0; i < M; ++i) {
+#ifdef QR_EXPERIMENT_NO_SEARCH  // cost-breakdown timing builds only (wrong results): the Hermite start as the root
+            const double y = quantile_start(t, i, search_target(t, nv, i));
+#else
             const double y = g_inv_search_wave<M>(t, *gmt, nv, i, ey[w], et[w], lane);
+#endif
             // noisemapper.pyx:503-515 in the reference's summation order (k < j, p[j], k > j).
-            // Straight-line: every lane computes both exponents (e, and e / 2 sigma^2 for k > j)
+            // Straight-line: every lane computes both exponents (e, and e / 2 sigma^2 for k > j;
+            // the missing / 2 sigma^2 for k < j is the reference's, noisemapper.pyx:503-507)
             // and selects -- the lanes of a wave hold different j, so a branch around the
             // division ran for nearly every k anyway, plus its exec-mask bookkeeping -- and
             // p[j] is the lane's own, loaded once per tile.
             double sum = 0;
+#ifdef QR_EXPERIMENT_NO_LLR  // cost-breakdown timing builds only (wrong results): no LLR sum
+            sum = pj + y * 1e-300;
+#else
 #pragma unroll kDemapUnroll
             for (int k = 0; k < M; ++k) {
                 const double ak = t.a[k];
                 const double e = (2 * y - ak - aj) * (ak - aj);
                 const double ed = div_two_s2(t, e);
-                const double arg = k < jj ? e : k == jj ? 1.0 : ed;
+                // (k == j: the term is p[j], the exp is not used, so its argument may be e)
+                const double arg = k > jj ? ed : e;
                 const double ex = g_exp_wave(arg, gt);
                 const double tk = ex * t.p[k];
                 sum += k == jj ? pj : tk;
             }
+#endif
             const double q = t.dF[i] / sum;
             int mi = i;
 #pragma unroll

@@ -274,8 +274,11 @@ __host__ __device__ __forceinline__ double g_exp_full(double x, const TT &T) {
 // exec-mask bookkeeping).  Same bits as g_exp_full for every input.
 template <class TT>
 __device__ __forceinline__ double g_exp_wave(double x, const TT &T) {
-    const uint32_t abstop = (g_hi(x) >> 20) & 0x7FFu;
-    const bool special = abstop - 0x3C9u >= 0x408u - 0x3C9u;
+    // lanes with |x| outside [2^-54, 512) or not finite (e_exp.c's special cases; abstop = the
+    // exponent field), as the compare's lane mask itself (llvm.amdgcn.icmp: a ballot of a bool
+    // materialised it first)
+    const uint64_t special_mask =
+        __builtin_amdgcn_uicmp(__builtin_amdgcn_ubfe(g_hi(x), 20, 11) - 0x3C9u, 0x408u - 0x3C9u, 35 /* uge */);
     double kd = __builtin_fma(x, kGxInvLn2N, kGxShift);
     const uint32_t ki = g_lo(kd);
     kd = kd - kGxShift;
@@ -291,9 +294,9 @@ __device__ __forceinline__ double g_exp_wave(double x, const TT &T) {
     const double r4 = r2 * r2;
     const double tmp = __builtin_fma(r4, p45, a);
     double res = __builtin_fma(scale, tmp, scale);
-    if (__builtin_amdgcn_ballot_w64(special)) {   // wave-uniform
-        if (special) res = g_exp_full(x, T);
-    }
+    // wave-uniform: a wave with a special lane runs the full routine on every lane (for the other
+    // lanes it is the same main path, the same bits)
+    if (special_mask) res = g_exp_full(x, T);
     return res;
 }
 

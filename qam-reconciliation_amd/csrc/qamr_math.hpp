@@ -417,9 +417,16 @@ QR_HD double hermite(double2 n0, double2 n1, double x) {
     return (n0.x * (1.0 + 2.0 * x) + n0.y * x) * (x1m * x1m) + (n1.x * (3.0 - 2.0 * x) + n1.y * x1m) * x2;
 }
 
-// Start point for the root of F_Y(y) = T in region k; NaN when out of the table.
+// Start point for the root of F_Y(y) = T in region k; NaN when out of the table.  (Device: the
+// nodes through global, not flat, loads -- a flat load also counts in lgkmcnt, so every LDS wait
+// of the wave would wait for it too.)
+#ifdef __HIP_DEVICE_COMPILE__
+typedef __attribute__((address_space(1))) const double2 qr_gdouble2;
+#else
+typedef const double2 qr_gdouble2;
+#endif
 QR_HD double quantile_start(const DemapTables &t, int k, double T) {
-    const double2 *Qk = t.quant + (size_t)k * kQStride;
+    qr_gdouble2 *Qk = (qr_gdouble2 *)(t.quant + (size_t)k * kQStride);
     const double u = (T - t.Fthr[k]) * t.inv_dF[k];
     const double w = (u < 0.5) ? u : 1.0 - u;
     if (w < 1.0 / (1 << kZoneOct)) {
@@ -427,7 +434,7 @@ QR_HD double quantile_start(const DemapTables &t, int k, double T) {
         if (!(x >= 0.0)) return __builtin_nan("");
         int j = (int)x;
         if (j > kZone - 2) j = kZone - 2;
-        const double2 *Z = (u < 0.5) ? Qk : Qk + kZone + kMid + 1;
+        qr_gdouble2 *Z = (u < 0.5) ? Qk : Qk + kZone + kMid + 1;
         return hermite(Z[j], Z[j + 1], x - j);
     }
     constexpr double kLo = 1.0 / (1 << kZoneOct), kScale = kMid / (1.0 - 2.0 * kLo);

@@ -141,16 +141,22 @@ def test_column_repack_vs_oracle(gpu, bps, snr, B, mi):
     _assert_timed_defaults()
     vid, cid, dec, pipe, b = _pipeline(bps, snr, B, seed=300 + int(10 * snr), max_iterations=mi)
     lappr = pipe.demap(b)
-    saved = _lib.tune_get("repack")
+    # the default; no repack; the variable sweeps never / always following the active-frame list
+    # (knob var_list_pct) with another row-mover grid
+    runs = [dict(), dict(repack=0), dict(var_list_pct=0), dict(var_list_pct=100, repack_grid=1024)]
+    names = ("repack", "var_list_pct", "repack_grid")
+    saved = {k: _lib.tune_get(k) for k in names}
     outs, stats = [], []
     try:
-        for rp in (1, 0):
-            _lib.tune_set("repack", rp)
+        for t in runs:
+            for k, v in saved.items():
+                _lib.tune_set(k, t.get(k, v))
             outs.append([x.clone() for x in pipe.decode(lappr, b)])
             torch.cuda.synchronize()
             stats.append(dec.repack_stats(pipe.ld, mi))
     finally:
-        _lib.tune_set("repack", saved)
+        for k, v in saved.items():
+            _lib.tune_set(k, v)
     (rep0, rep1), (w0, w1) = stats[0]
     assert rep0 + rep1 > 0, stats[0]                  # the device repacked
     assert min(w0, w1) < pipe.ld // 2, stats[0]
