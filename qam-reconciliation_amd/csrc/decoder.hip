@@ -38,6 +38,8 @@
 namespace qr {
 
 enum CheckMode { kFirst = 0, kNormal = 1, kParityOnly = 2 };
+#define QR_STR2(x) #x
+#define QR_STR(x) QR_STR2(x)
 
 // Device-side index checks of the debug build (make -C csrc DEBUG=1 -> qamr/libqamr_debug.so,
 // QR_DEBUG_ASSERT=1; SURVEY.md 5 -- the reference turns bounds checks off, decoder.pyx:181,240,
@@ -180,6 +182,11 @@ struct CheckArgs {
     const double *post_w;
     const uint8_t *synd_w[2];
     double *c2v_alt;
+    // set by select_range: 1 for the first sweep after a repack (its messages are read from the
+    // old column set at the frames' old columns, c2v_rd / the list; everything else is read and
+    // written in the new columns, see k_repack_rows)
+    int transit;
+    const double *c2v_rd;
 };
 
 // One variable sweep over the frame columns [f_off, f_off + ny*ft).
@@ -205,10 +212,7 @@ struct VarArgs {
     const double *lappr_w[2];
     double *post_w;
     const double *c2v_alt;
-    // knob var_list_pct: the sweep follows the active-frame list only when the running frames fill
-    // at most this percentage of the range's columns (else lane = column, stopped frames skipped
-    // by their flag); 100 = always
-    int list_pct;
+    int transit;  // as CheckArgs (set by select_range); in transit c2v is the old column set
 };
 
 // The state of one frame range of the two-stream schedule, in device memory (the workspace's
@@ -217,7 +221,11 @@ struct VarArgs {
 // first columns), how many repacks it went through, and which of the work set's two column sets
 // (messages, LAPPRs, syndrome bits) holds it: a repack gathers the running columns of one set
 // into the other, so no column is overwritten while another thread may still read it.
-enum RangeSelField { kSelOn = 0, kSelW = 1, kSelRepacks = 2, kSelArrive = 3, kSelBuf = 4, kSelInts = 5 };
+// kSelTransit: the range was repacked at its last decision point and the sweeps that follow it
+// (its variable sweep, then its check sweeps) have not all run yet: their messages still live in
+// the old column set, at the frames' old columns (the active-frame list, which the commit leaves
+// as it is until the next status launch rebuilds it).
+enum RangeSelField { kSelOn = 0, kSelW = 1, kSelRepacks = 2, kSelArrive = 3, kSelBuf = 4, kSelTransit = 5, kSelInts = 6 };
 
 // Kernel-uniform: the arrays a range's launch reads once the device has repacked the range.
 __device__ __forceinline__ void select_range(CheckArgs &a) {
@@ -225,7 +233,10 @@ __device__ __forceinline__ void select_range(CheckArgs &a) {
         const int b = sld(a.sel + kSelBuf);
         a.post = a.post_w;
         a.synd = b ? a.synd_w[1] : a.synd_w[0];  // (selects: a dynamic index would put a in scratch)
-        if (b) a.c2v = a.c2v_alt;
+        double *const c0 = a.c2v, *const c1 = a.c2v_alt;
+        a.c2v = b ? c1 : c0;
+        a.transit = sld(a.sel + kSelTransit);
+        a.c2v_rd = a.transit ? (b ? c0 : c1) : a.c2v;
     }
 }
 __device__ __forceinline__ void select_range(VarArgs &a) {
@@ -233,7 +244,8 @@ __device__ __forceinline__ void select_range(VarArgs &a) {
         const int b = sld(a.sel + kSelBuf);
         a.lappr = b ? a.lappr_w[1] : a.lappr_w[0];
         a.post = a.post_w;
-        if (b) a.c2v = a.c2v_alt;
+        a.transit = sld(a.sel + kSelTransit);
+        if (a.transit ? !b : b) a.c2v = a.c2v_alt;  // transit: the old set
     }
 }
 
@@ -262,7 +274,7 @@ __device__ __forceinline__ int lane_frame(const int32_t *alist, const int32_t *a
 // The gathered posteriors of check j+1 are issued before the arithmetic of check j on the
 // unpacked paths (the packed strict update needs those registers: with the prefetch it runs
 // at 3 waves/SIMD, 142 VGPRs); the own (streamed, row-contiguous) messages are loaded on use.
-template <int D, int MODE, bool NT>
+template <int D, int MODE, bool NT, bool TRANSIT = false>
 struct CheckIn {
     double p[D], c[D];
     int base;
@@ -276,11 +288,13 @@ struct CheckIn {
 #pragma unroll
         for (int i = 0; i < D; ++i) p[i] = ld_row<false>(row_ptr(a.post, sld(a.chk_var + base + i), ld), b8, ld);
     }
-    __device__ __forceinline__ void load_c(const CheckArgs &a, int f) {
+    // fc: the frame's column of its messages (in transit its old column, c2v_rd the old set)
+    __device__ __forceinline__ void load_c(const CheckArgs &a, int fc) {
         if (MODE != kNormal) return;
-        const uint32_t b8 = (uint32_t)f * 8u;
+        const uint32_t b8 = (uint32_t)fc * 8u;
+        const double *c2v = TRANSIT ? a.c2v_rd : a.c2v;
 #pragma unroll
-        for (int i = 0; i < D; ++i) c[i] = ld_row<NT>(row_ptr(a.c2v, sld(a.chk_edge + base + i), a.ld), b8, a.ld);
+        for (int i = 0; i < D; ++i) c[i] = ld_row<NT>(row_ptr(c2v, sld(a.chk_edge + base + i), a.ld), b8, a.ld);
     }
 };
 
@@ -348,13 +362,17 @@ __device__ __forceinline__ void check_exact(const CheckArgs &a, const double (&m
 // decoder.pyx:322-369 (F/B recursion) with the parity test of decoder.pyx:235-257
 // fused on the posteriors it gathers anyway.  Unpacked paths are software-pipelined: the
 // posterior gathers of check j+1 are issued before the box-plus arithmetic of check j.
-template <int D, int MODE, bool NT, bool FIN = false>
+template <int D, int MODE, bool NT, bool FIN = false, bool TRANSIT = false>
 __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, unsigned by, int per,
                                             const GlibcTablesBP &tab, double *hb) {
     const int ft = 1 << a.g.lft;
     const int nsub = 256 >> a.g.lft;
     bool live;
-    const int f = lane_frame(a.alist, a.acount, a.f_off, (int)(by << a.g.lft) + (threadIdx.x & (ft - 1)), live);
+    const int lp = (int)(by << a.g.lft) + (threadIdx.x & (ft - 1));
+    const int fl = lane_frame(a.alist, a.acount, a.f_off, lp, live);
+    // TRANSIT (the first check sweep after a repack): the lane's frame sits in column f_off + lp of
+    // the new set; only its old messages are still at its listed (old) column fl
+    const int f = TRANSIT ? a.f_off + lp : fl;
     const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> a.g.lft);
     // Waves whose 64 frames all stopped leave; in a partly stopped wave the stopped
     // lanes run along (no divergent exit, so the loop state stays scalar): their
@@ -368,11 +386,11 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
     uint32_t bad = 0;
     const auto K = GlibcK::pinned();
     constexpr bool kPrefetch = !kPacked<D>;
-    CheckIn<D, MODE, NT> nx;
+    CheckIn<D, MODE, NT, TRANSIT> nx;
     nx.load(a, ci, f);
     for (int j = 0; j < per; ++j) {
         // consume check j's inputs (m, parity) before its registers take check j+1's
-        nx.load_c(a, f);
+        nx.load_c(a, TRANSIT ? fl : f);
         uint32_t par = nx.sb;
         double m[D];
 #pragma unroll
@@ -402,13 +420,18 @@ __device__ __forceinline__ void check_block(const CheckArgs &a, unsigned bx, uns
 // INIT: the first sweep with c2v == 0 (decoder.pyx:408,420-421): lappr + 0.0 for
 // frames still decoding; frames already successful at iteration 0 get a plain
 // copy of their input (decoder.pyx:404).
-template <bool INIT, bool NT>
+// TRANSIT (the first variable sweep after a repack): the frame's LAPPRs and posterior are in
+// column f_off + lp of the new set, its messages still at its listed (old) column of the old set.
+template <bool INIT, bool NT, bool TRANSIT = false>
 __device__ __forceinline__ void var_block(const VarArgs &a, unsigned bx, unsigned by) {
     const int ft = 1 << a.g.lft;
     const int nsub = 256 >> a.g.lft;
     const int ld = a.ld;
     bool live;
-    const int f = lane_frame(a.alist, a.acount, a.f_off, (int)(by << a.g.lft) + (threadIdx.x & (ft - 1)), live);
+    const int lp = (int)(by << a.g.lft) + (threadIdx.x & (ft - 1));
+    const int fl = lane_frame(a.alist, a.acount, a.f_off, lp, live);
+    const int f = TRANSIT ? a.f_off + lp : fl;
+    const int fc = TRANSIT ? fl : f;
     const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> a.g.lft);
     const bool act = a.active[f] != 0;
     if (!live || (!INIT && !act)) return;
@@ -423,7 +446,7 @@ __device__ __forceinline__ void var_block(const VarArgs &a, unsigned bx, unsigne
             big |= !(__builtin_fabs(p) < a.fin_bound);
             if (act && e > b) p = p + 0.0;
         } else {
-            for (int k = b; k < e; ++k) p += ld_msg<NT>(&a.c2v[(size_t)sld(a.var_edge + k) * ld + f]);
+            for (int k = b; k < e; ++k) p += ld_msg<NT>(&a.c2v[(size_t)sld(a.var_edge + k) * ld + fc]);
         }
         a.post[(size_t)v * ld + f] = p;
     }
@@ -444,7 +467,7 @@ constexpr int kNarrowNodes = 256 / kNarrowFrames;
 constexpr int kNarrowW = 64;
 
 __device__ __forceinline__ bool range_narrow(const int32_t *sel, const int32_t *acount) {
-    return sel && acount && sld(sel + kSelOn) && sld(sel + kSelW) <= kNarrowW;
+    return sel && acount && sld(sel + kSelOn) && sld(sel + kSelW) <= kNarrowW && !sld(sel + kSelTransit);
 }
 // Tasks of a narrow sweep over n nodes: (node block, frame group) pairs, frame group fastest, the
 // group count (<= 4) rounded up to 2^lg so that a task splits with a shift and a mask (32-bit task
@@ -563,6 +586,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
     ClkScope clk(D == 7 && MODE == kNormal, g_clk, g_wgt);
 #endif
     if (MODE != kParityOnly) stage_glibc_tables(&tab, a.gglibc);
+    if constexpr (MODE == kNormal && kPacked<D>) {
+        if (a.transit) {  // kernel-uniform: the first sweep after a repack (NaN-preserving clamp)
+            check_block<D, MODE, NT, false, true>(a, bx, by, per, tab, hb);
+            return;
+        }
+    }
     if constexpr (MODE != kParityOnly && kPacked<D>) {
         if (a.finite && sld(a.finite)) {  // kernel-uniform: one of the two bodies runs
             check_block<D, MODE, NT, true>(a, bx, by, per, tab, hb);
@@ -572,28 +601,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 8))
     check_block<D, MODE, NT, false>(a, bx, by, per, tab, hb);
 }
 
+template <bool INIT, bool NT, bool TRANSIT>
+__device__ __forceinline__ void var_sweep_body(const VarArgs &a);
+
 template <bool INIT, bool NT>
 __global__ void __launch_bounds__(256) k_var(VarArgs a) {
+#ifdef QR_EXPERIMENT_VAR_VGPR  // register-rule probe builds only: allocate this many VGPRs (e.g. 24)
+    __asm__ volatile("" ::: "v" QR_STR(QR_EXPERIMENT_VAR_VGPR_LAST));
+#endif
     select_range(a);
     if (!INIT && range_narrow(a.sel, a.acount)) {  // kernel-uniform
         var_narrow_sweep(a);
         return;
     }
-    // A partly stopped range: the list maps the lanes of a wave to scattered columns, so each wave
-    // reads ~1.5x the cache lines of a dense wave for the same bytes, and this sweep is bound by
-    // those lines (MI355X, 4-PAM 4.0 dB: 4.4-4.8 ms per sweep of a range with ~70 % of its frames
-    // running, against 3.5 ms dense; the check sweep beside it, VALU-bound, gains from the list).
-    // While most columns still run, sweep the columns themselves (kernel-uniform): the stopped
-    // frames' lanes load and skip their store (their flag), every wave reads 64 consecutive columns.
-    if (!INIT && a.alist && a.list_pct < 100) {
-        const int cnt = sld(a.acount);
-        const int w = (a.sel && sld(a.sel + kSelOn)) ? sld(a.sel + kSelW) : (int)(a.nby << a.g.lft);
-        if ((int64_t)cnt * 100 > (int64_t)w * a.list_pct) {
-            a.alist = nullptr;
-            a.acount = nullptr;
-            a.nby = min(a.nby, (unsigned)((w + (1 << a.g.lft) - 1) >> a.g.lft));
-        }
-    }
+    if (!INIT && a.transit) var_sweep_body<INIT, NT, true>(a);  // kernel-uniform
+    else var_sweep_body<INIT, NT, false>(a);
+}
+
+template <bool INIT, bool NT, bool TRANSIT>
+__device__ __forceinline__ void var_sweep_body(const VarArgs &a) {
     if (a.gs) {  // capped grid: tile t = (bx fastest, by), the grid's blocks sweep a moving window
         unsigned ny = a.nby, stride = gridDim.x;
         if (a.boost > 1) {
@@ -611,12 +637,12 @@ __global__ void __launch_bounds__(256) k_var(VarArgs a) {
         const unsigned n = a.nbx * ny;
         for (unsigned t = blockIdx.x; t < n; t += stride) {
             const unsigned by = t / a.nbx, bx = t - by * a.nbx;
-            if (frames_block_live(a.acount, by, a.g.lft)) var_block<INIT, NT>(a, bx, by);
+            if (frames_block_live(a.acount, by, a.g.lft)) var_block<INIT, NT, TRANSIT>(a, bx, by);
         }
         return;
     }
     if (!frames_block_live(a.acount, blockIdx.y, a.g.lft)) return;
-    var_block<INIT, NT>(a, blockIdx.x, blockIdx.y);
+    var_block<INIT, NT, TRANSIT>(a, blockIdx.x, blockIdx.y);
 }
 
 
@@ -1111,7 +1137,12 @@ __global__ void __launch_bounds__(1024) k_compact(int f0, int f1, uint8_t *__res
         base += tot;
         __syncthreads();  // wsum is rewritten by the next chunk
     }
-    if (threadIdx.x == 0) *count = base;
+    if (threadIdx.x == 0) {
+        *count = base;
+        // the status launch after a range's check sweep: the sweeps of a repack's transition have
+        // all run (variable sweep, side and main check sweeps), the list is in the new columns
+        if (STATUS && sel) const_cast<int32_t *>(sel)[kSelTransit] = 0;
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1259,8 +1290,9 @@ __device__ __forceinline__ void gather_rows(const TS *src, TD *dst, int64_t n, i
     }
 }
 
-// The commit of a repack (by the workgroup of k_repack_rows that finishes last): frame ids, list,
-// active flags and the RangeSel (now in column set nb).
+// The commit of a repack (by the workgroup of k_repack_rows that finishes last): frame ids, active
+// flags and the RangeSel (now in column set nb, in transit).  The list keeps the frames' old
+// columns: the transition sweeps read the messages there; the next status launch rebuilds it.
 __device__ __forceinline__ void repack_commit(const RepackArgs &r, int cnt, int w, int w_new, bool on, int nb) {
     const int f0 = r.f0;
     for (int p0 = 0; p0 < cnt; p0 += kRepackThreads) {
@@ -1274,7 +1306,6 @@ __device__ __forceinline__ void repack_commit(const RepackArgs &r, int cnt, int 
         loads_done_barrier();  // fid_w is compacted in place: every read of this chunk first
         if (p < cnt) {
             r.fid_w[f0 + p] = id;
-            r.list[f0 + p] = f0 + p;
             r.active[f0 + p] = 1;
         }
     }
@@ -1288,6 +1319,7 @@ __device__ __forceinline__ void repack_commit(const RepackArgs &r, int cnt, int 
         r.sel[kSelRepacks] += 1;
         r.sel[kSelArrive] = 0;
         r.sel[kSelBuf] = nb;
+        r.sel[kSelTransit] = 1;
     }
 }
 
@@ -1337,8 +1369,8 @@ __global__ void __launch_bounds__(kRepackThreads) k_repack_rows(RepackArgs r) {
             src_el[u] = ok ? (uint32_t)(j * ld + r.list[f0 + p0 + q]) * 8u : kRepackNone;
             dst_el[u] = ok ? (uint32_t)(j * ld + f0 + p0 + q) * 8u : kRepackNone;
         }
-        // source set b, destination set nb (selects, not dynamic indices into the kernel arguments)
-        gather_rows<double, double>(b ? r.c2v[1] : r.c2v[0], nb ? r.c2v[1] : r.c2v[0], r.E, ld, ld, rg, src_el, dst_el);
+        // source set b, destination set nb (selects, not dynamic indices into the kernel arguments);
+        // the messages are not moved here: the transition sweeps read them at the old columns
         gather_rows<double, double>(!on ? r.lappr_in : b ? r.lappr_w[1] : r.lappr_w[0], nb ? r.lappr_w[1] : r.lappr_w[0],
                                     r.V, ld, ld, rg, src_el, dst_el);
         gather_rows<uint8_t, uint8_t>(!on ? r.synd_in : b ? r.synd_w[1] : r.synd_w[0], nb ? r.synd_w[1] : r.synd_w[0],
@@ -1377,7 +1409,7 @@ struct DecodeWs {
     int32_t *alist;  // active-frame lists of the frame ranges (ld entries)
     int32_t *acount; // their lengths: [0] range starting at frame 0, [1] the second half;
                      // [2] the finite flag of the input LAPPRs (first variable sweep);
-                     // [4, 12) the two ranges' RangeSel (rsel)
+                     // [4, 16) the two ranges' RangeSel (rsel)
     int32_t *rsel;
     // the work set of the column repack (k_repack_rows, run_split2): posteriors and the frame id
     // of each column of the repacked ranges, and two column sets of LAPPRs and syndrome bits (and
@@ -1463,7 +1495,7 @@ struct Tuning {
     std::atomic<int> check_ft{128}, check_per{16}, var_ft{128}, var_per{8}, nt{1}, split{3},
         lds_pad_kb{0}, compact{1}, side{1}, min_blocks{2048}, split_min_blocks{1024}, var_pace{28},
         check_tail{4}, fused_iter{1}, iter_streams{2}, var_boost{4}, resident{1}, repack{1},
-        repack_pct{50}, repack_grid{512}, var_list_pct{100};
+        repack_pct{80}, repack_grid{512};
 };
 static Tuning g_tune;
 
@@ -1548,6 +1580,8 @@ struct Plan {
         a.synd_w[0] = w.rs.synd[0];
         a.synd_w[1] = w.rs.synd[1];
         a.c2v_alt = w.rs.c2v_alt;
+        a.transit = 0;
+        a.c2v_rd = a.c2v;
         return a;
     }
     VarArgs var_args(int f0, int f1) const {
@@ -1576,7 +1610,7 @@ struct Plan {
         a.lappr_w[1] = w.rs.lappr[1];
         a.post_w = w.rs.post;
         a.c2v_alt = w.rs.c2v_alt;
-        a.list_pct = std::clamp(g_tune.var_list_pct.load(), 0, 100);
+        a.transit = 0;
         return a;
     }
 };
@@ -1915,12 +1949,13 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
         if (!side) return (int)QR_OK;
         return launch_checks<kNormal>(V, P.post, row(t - 1), k * h, (k + 1) * h, big);
     };
-    // range k's variable sweep, preceded by its repack decision point (the status launch it waits
-    // for wrote the count the device decides on); the copies run under the other range's check
-    // launch
-    auto var_sweep = [&](int k) {
+    // range k's variable sweep t, preceded by its repack decision point (the status launch it
+    // waits for wrote the count the device decides on); the copies run under the other range's
+    // check launch.  No decision before the last variable sweep: a repack's transition ends with
+    // the check sweep that follows it (the final parity sweep reads the columns of the list).
+    auto var_sweep = [&](int k, int t) {
         const int f0 = k * h;
-        if (rp) {
+        if (rp && t < max_it) {
             if (int rc0 = launch_repack(V, f0, h)) return rc0;
         }
         return launch_var<false>(V, f0, f0 + h);
@@ -1935,7 +1970,7 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
     QR_HIP(hipEventRecord(cA, P.s));
     for (int t = 1; t <= max_it; ++t) {
         QR_HIP(hipStreamWaitEvent(V.s, cA, 0));
-        if ((rc = var_sweep(0))) return rc;
+        if ((rc = var_sweep(0, t))) return rc;
         if (t < max_it && (rc = checks_side(t + 1, 0))) return rc;
         QR_HIP(hipEventRecord(vA, V.s));
         if (t == 1) {
@@ -1953,7 +1988,7 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
             QR_HIP(hipEventRecord(cA, P.s));
         }
         QR_HIP(hipStreamWaitEvent(V.s, cB, 0));
-        if ((rc = var_sweep(1))) return rc;
+        if ((rc = var_sweep(1, t))) return rc;
         if (t < max_it && (rc = checks_side(t + 1, 1))) return rc;
         QR_HIP(hipEventRecord(vB, V.s));
     }
@@ -2404,7 +2439,6 @@ static std::atomic<int> *tune_knob(const char *name) {
         {"fused_iter", &g_tune.fused_iter}, {"iter_streams", &g_tune.iter_streams},
         {"resident", &g_tune.resident},   {"repack", &g_tune.repack},
         {"repack_pct", &g_tune.repack_pct}, {"repack_grid", &g_tune.repack_grid},
-        {"var_list_pct", &g_tune.var_list_pct},
     };
     const std::string n = name ? name : "";
     for (const auto &k : knobs)

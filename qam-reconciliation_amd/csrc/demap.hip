@@ -184,8 +184,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
                 const double ak = t.a[k];
                 const double e = (2 * y - ak - aj) * (ak - aj);
                 const double ed = div_two_s2(t, e);
-                // (k == j: the term is p[j], the exp is not used, so its argument may be e)
-                const double arg = k > jj ? ed : e;
+                // k == j: the term is p[j] and the exp is not used, but its argument must stay off
+                // exp's special cases -- e is 0 there, and one such lane sends the whole wave
+                // through the full routine at every k (measured 40.1 -> 46.5 ms)
+                const double arg = k < jj ? e : k == jj ? 1.0 : ed;
                 const double ex = g_exp_wave(arg, gt);
                 const double tk = ex * t.p[k];
                 sum += k == jj ? pj : tk;

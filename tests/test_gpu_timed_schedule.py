@@ -131,20 +131,22 @@ def test_column_repack_vs_oracle(gpu, bps, snr, B, mi):
     batches of its converging operating points (BENCH op_dvbs2_4pam_4.0dB /
     op_dvbs2_16pam_14.5dB): every frame identical to the run with no repack at all, the frames
     that ran longest -- the ones that went through the repacks -- and frames spread over both
-    ranges bit-exact against the oracle, and the device did repack.  On the bench's 4-PAM
-    4.0 dB batch a range repacks more than once (column set 1 -> 0 as well as 0 -> 1) and ends
-    at most 64 columns wide, so its last iterations ran the narrow sweeps (lanes = node x
-    frame, check_narrow / var_narrow_sweep) (reference: decoder.pyx:424-436)."""
+    ranges bit-exact against the oracle, and the device did repack.  Each repack's first variable
+    and check sweeps read the messages at the frames' old columns of the old set (the transition:
+    k_repack_rows moves no message).  On the bench's 4-PAM 4.0 dB batch a range repacks more than
+    once (column set 1 -> 0 as well as 0 -> 1) and ends at most 64 columns wide, so its last
+    iterations ran the narrow sweeps (lanes = node x frame, check_narrow / var_narrow_sweep)
+    (reference: decoder.pyx:424-436)."""
     import torch
     from qamr import _lib
 
     _assert_timed_defaults()
     vid, cid, dec, pipe, b = _pipeline(bps, snr, B, seed=300 + int(10 * snr), max_iterations=mi)
     lappr = pipe.demap(b)
-    # the default; no repack; the variable sweeps never / always following the active-frame list
-    # (knob var_list_pct) with another row-mover grid
-    runs = [dict(), dict(repack=0), dict(var_list_pct=0), dict(var_list_pct=100, repack_grid=1024)]
-    names = ("repack", "var_list_pct", "repack_grid")
+    # the default (repack_pct 80: repacks early and often, transitions at consecutive decision
+    # points); no repack; another row-mover grid; repacks at 50 %
+    runs = [dict(), dict(repack=0), dict(repack_grid=1024), dict(repack_pct=50)]
+    names = ("repack", "repack_pct", "repack_grid")
     saved = {k: _lib.tune_get(k) for k in names}
     outs, stats = [], []
     try:
@@ -157,9 +159,11 @@ def test_column_repack_vs_oracle(gpu, bps, snr, B, mi):
     finally:
         for k, v in saved.items():
             _lib.tune_set(k, v)
+    # the device repacked (no repack is decided before the last variable sweep: its transition
+    # would end in the final parity sweep; with max_iterations 22 a 50 % threshold is first met there)
     (rep0, rep1), (w0, w1) = stats[0]
-    assert rep0 + rep1 > 0, stats[0]                  # the device repacked
-    assert min(w0, w1) < pipe.ld // 2, stats[0]
+    assert rep0 + rep1 > 0, stats
+    assert min(w0, w1) < pipe.ld // 2, stats
     assert stats[1] == ((0, 0), (pipe.ld // 2, pipe.ld // 2))  # repack off: never
     if (bps, snr, B) == (2, 4.0, 4096):
         assert max(rep0, rep1) >= 2, stats[0]  # both directions between the column sets
