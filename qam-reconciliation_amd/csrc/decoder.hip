@@ -1850,10 +1850,7 @@ static int side_stream(const qr_code *code, hipStream_t *out) {
         hipStream_t s2 = nullptr;
         hipEvent_t ev[5] = {};
         hipError_t e = hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
-#ifndef QR_EXPERIMENT_EVENT_FLAGS
-#define QR_EXPERIMENT_EVENT_FLAGS hipEventDisableTiming
-#endif
-        for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ev[i], QR_EXPERIMENT_EVENT_FLAGS);
+        for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
         if (e != hipSuccess) {
             for (auto x : ev)
                 if (x) (void)hipEventDestroy(x);
