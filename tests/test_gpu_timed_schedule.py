@@ -173,7 +173,10 @@ def test_column_repack_vs_oracle(gpu, bps, snr, B, mi):
         assert torch.equal(s1, s0) and torch.equal(i1, i0)
         assert torch.equal(f1[:, :B].view(torch.int64), f0[:, :B].view(torch.int64))
     its = i1.cpu().numpy()
-    cols = np.unique(np.r_[np.argsort(-its, kind="stable")[:8], _cols(B, 8)])
+    # the bench's own 4.0 dB batch: 64 frames more against the oracle, spread over both ranges
+    # (every column set and transition a frame can go through before it stops)
+    nspread = 72 if (bps, snr, B) == (2, 4.0, 4096) else 8
+    cols = np.unique(np.r_[np.argsort(-its, kind="stable")[:8], _cols(B, nspread)])
     ct = torch.as_tensor(cols, device=lappr.device)
     L = lappr[:, ct].T.contiguous().cpu().numpy()
     Sy = b.synd[:, ct].T.contiguous().cpu().numpy()
