@@ -96,9 +96,10 @@ QR_API int qr_code_info(const qr_code *code, int64_t *vnum, int64_t *cnum, int64
 /* Device workspace (bytes) for qr_decode_batch_device at leading dim ld and
  * max_iterations (edge messages E*ld fp64 + per-frame flags; with tuning knob "repack" on
  * (default) and ld % 512 == 0, plus the column-repack work set: posteriors, frame ids and two
- * column sets of messages, LAPPRs and syndrome bits that consecutive repacks gather into in
- * turn, (8E + 24V + 2C + 4)*ld bytes -- a workspace without it runs the same decode without
- * the repack). */
+ * column sets of messages, LAPPRs and syndrome bits used in turn by consecutive repacks (the
+ * repack gathers LAPPRs and syndrome bits, the check sweep after it writes the messages),
+ * (8E + 24V + 2C + 4)*ld bytes -- a workspace without it runs the same decode without the
+ * repack). */
 QR_API int qr_decode_workspace_size(const qr_code *code, int32_t ld, int32_t max_iterations, size_t *bytes);
 
 /* Batched Decoder._decode (decoder.pyx:391-436) of B independent frames.
