@@ -5,9 +5,10 @@ index checks (decoder.hip QR_DCHECK) on the column repack's active-frame list, f
 slots (k_repack_rows, k_repack_output), the active-frame list writes (k_compact) and reads
 (lane_frame), the narrow sweeps' lane -> (node, frame) mapping, and the frame-resident decode's LDS
 posterior and message indices (k_resident).  This test runs the repack parity tests (the bench's
-4-PAM 4.0 dB B = 4096 batch: repacks in both directions between the column sets, narrow sweeps) and
-the frame-resident parity tests (configs[1] full batch, ragged batch shapes) in a child process on
-that library; conftest's autouse fixture fails any test after which a device check failed."""
+4-PAM 4.0 dB and 16-PAM 14.5 dB B = 4096 batches: repacks in both directions between the column
+sets, transitions, narrow sweeps; a short max_iterations; the captured decode), the schedule and
+tuning invariance test, and the frame-resident parity tests (configs[1] full batch, ragged batch
+shapes) in a child process on that library; conftest's autouse fixture fails any test after which a device check failed."""
 import os
 import subprocess
 import sys
@@ -21,8 +22,12 @@ DEBUG_LIB = os.path.join(ROOT, "qam-reconciliation_amd", "qamr", "libqamr_debug.
 
 CASES = [
     "tests/test_gpu_timed_schedule.py::test_column_repack_vs_oracle[2-4.0-4096-50]",
+    "tests/test_gpu_timed_schedule.py::test_column_repack_vs_oracle[4-14.5-4096-50]",
     "tests/test_gpu_timed_schedule.py::test_column_repack_vs_oracle[4-14.5-1024-50]",
+    "tests/test_gpu_timed_schedule.py::test_column_repack_vs_oracle[2-4.0-1024-22]",
+    "tests/test_gpu_timed_schedule.py::test_repack_decode_is_asynchronous_and_capturable",
     "tests/test_gpu_timed_schedule.py::test_repack_stats_after_resident_decode",
+    "tests/test_gpu_properties.py::test_schedule_and_tuning_invariance",
     "tests/test_gpu_parity_edges.py::test_configs1_full_batch_vs_oracle",
     "tests/test_gpu_parity_edges.py::test_resident_batch_shapes_vs_oracle",
 ]
@@ -35,4 +40,4 @@ def test_debug_build_device_checks(gpu):
                        env=env, capture_output=True, text=True, timeout=900)
     tail = (r.stdout + r.stderr)[-3000:]
     assert r.returncode == 0, tail
-    assert "8 passed" in r.stdout, tail  # the 5 cases above (the batch-shape test has 4 parameters)
+    assert "12 passed" in r.stdout, tail  # the 9 cases above (the batch-shape test has 4 parameters)
