@@ -1387,16 +1387,25 @@ __global__ void __launch_bounds__(kRepackThreads) k_repack_rows(RepackArgs r) {
 }
 
 
-__global__ void k_repack_output(int64_t rows, int f0, int ld, const int32_t *sel, const int32_t *__restrict__ fid_w,
-                                const double *__restrict__ post_w, double *__restrict__ out_post) {
+// The range's final width is known only here, so the work is (row, 64-column chunk) units, one
+// per wave, walked grid-stride by every wave of the grid: a narrow range (the usual end of a
+// converging one) still gets the whole grid (one unit per wave, rows in parallel).
+__global__ void __launch_bounds__(256) k_repack_output(int64_t rows, int f0, int ld, const int32_t *sel,
+                                                       const int32_t *__restrict__ fid_w,
+                                                       const double *__restrict__ post_w, double *__restrict__ out_post) {
     if (!sld(sel + kSelOn)) return;  // kernel-uniform: never repacked (the output is the posteriors)
     const int w = sld(sel + kSelW);
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= w) return;
-    const int id = fid_w[f0 + q];
-    if (id < 0) return;
-    QR_DCHECK(id < ld, kDbgRepackFid, id, q);
-    for (int64_t v = blockIdx.y; v < rows; v += gridDim.y) out_post[(size_t)v * ld + id] = post_w[(size_t)v * ld + f0 + q];
+    const int nq = (w + 63) >> 6;
+    const int lane = (int)(threadIdx.x & 63u);
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6), units = rows * nq;
+    for (int64_t u = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); u < units; u += nwaves) {
+        const int64_t v = u / nq;
+        const int q = (int)(u - v * nq) * 64 + lane;
+        const int id = q < w ? fid_w[f0 + q] : -1;
+        if (id < 0) continue;
+        QR_DCHECK(id < ld, kDbgRepackFid, id, q);
+        out_post[(size_t)v * ld + id] = post_w[(size_t)v * ld + f0 + q];
+    }
 }
 
 // ------------------------------------------------------------------ launch
@@ -2007,8 +2016,7 @@ static int run_split2(const Plan &P, int max_it, bool *finalized) {
         if ((rc = launch_checks<kParityOnly>(F, P.post, unsat_last, f0, f0 + h))) return rc;
         if ((rc = launch_status(F, f0, f0 + h, max_it, 1, max_it, unsat_last))) return rc;
         ProfScope ps("repack_out", P.s);
-        k_repack_output<<<dim3((unsigned)(h + 255) / 256, (unsigned)std::min<int64_t>(code->V, 2048)), 256, 0, P.s>>>(
-            code->V, f0, ld, F.sel_of(f0), P.w.rs.fid, P.w.rs.post, P.post);
+        k_repack_output<<<4096, 256, 0, P.s>>>(code->V, f0, ld, F.sel_of(f0), P.w.rs.fid, P.w.rs.post, P.post);
         QR_LAUNCH_CHECK();
     }
     *finalized = true;
