@@ -144,8 +144,9 @@ def test_column_repack_vs_oracle(gpu, bps, snr, B, mi):
     vid, cid, dec, pipe, b = _pipeline(bps, snr, B, seed=300 + int(10 * snr), max_iterations=mi)
     lappr = pipe.demap(b)
     # the default (repack_pct 80: repacks early and often, transitions at consecutive decision
-    # points); no repack; another row-mover grid; repacks at 50 %
-    runs = [dict(), dict(repack=0), dict(repack_grid=1024), dict(repack_pct=50)]
+    # points; row-move grid 128); no repack; an odd 7-workgroup grid (each walks many row groups);
+    # repacks at 50 % with a 1 024-workgroup grid
+    runs = [dict(), dict(repack=0), dict(repack_grid=7), dict(repack_pct=50, repack_grid=1024)]
     names = ("repack", "repack_pct", "repack_grid")
     saved = {k: _lib.tune_get(k) for k in names}
     outs, stats = [], []
